@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py — raytracer-gamma hot path on MI355X: Mpixels/s of the per-pixel
+Whitted raytrace (librtg.so HIP kernel) on BASELINE.json's configs[2] workload.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+  torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU)
+
+A step renders ONE full frame (3840x2160, 16 spheres, 3 lights, depth 5 =
+RTSTACK_MAXSIZE 6, 3x3 supersampling = 74.6 M primary rays) of the seeded
+synthetic scene from a scene already resident in HBM.  With
+N > 1 the frame's rows are dealt row-cyclically (16-row blocks) to the ranks
+and rank 0 gathers them with one RCCL gather over xGMI and restores row order
+on the device, so the step ends with the whole frame in rank 0's HBM (strong
+scaling: fixed frame).  Rank 0 prints one JSON line.
+
+Also reported: the kernel roofline (FP32 VALU; algorithmic work = the
+reference's ray-sphere tests x 25 flops), the reference CPU
+path timed on a bounded row sample on this host (cpu_baseline), and parity of
+the produced frame/PPM against the reference's golden hashes.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # first: owns the HIP runtime librtg.so binds to (see rtg_amd)
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytracer-gamma_amd"))
+import rtg_amd as R  # noqa: E402
+from rtg_amd import dist as rdist  # noqa: E402
+
+METRIC = "Mpixels/s (primary rays) + frame ms at WxH, depth D; PPM max-abs-diff vs CPU"
+GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.json")
+CONFIGS = {  # name: (W, H, spheres, lights, depth)  — BASELINE.json configs
+    "c1": (640, 480, 4, 1, 1),
+    "c2": (1920, 1080, 8, 2, 3),
+    "c3": (3840, 2160, 16, 3, 5),
+    "c4": (7680, 4320, 32, 4, 5),
+    "c5": (3840, 2160, 1024, 4, 7),
+}
+# FP32 VALU issue peak for non-FMA ops: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
+# (MI355X_MICROARCH.md's 157.3 TFLOPS FP32-vector spec counts an FMA as two
+# flops; parity with the reference forbids contraction, so adds and muls issue
+# separately and 78.6 T op/s is the ceiling for this kernel's op mix.)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0
+FLOPS_PER_TEST = 25  # raySphere pre-branch ops, SURVEY.md §8d
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def canon_md5(fb: np.ndarray) -> str:
+    b = fb.view(np.uint32).copy()
+    b[np.isnan(fb)] = 0xFFC00000
+    return hashlib.md5(b.tobytes()).hexdigest()
+
+
+def cpu_baseline(name, sph, lg, W, H, S, budget_s):
+    """Reference CPU path (oracle/_ref, compiled from the reference's
+    raytracer.h) on one host thread over a strided row sample of the same
+    frame; falls back to the C restatement if the reference build is absent."""
+    ref = os.path.join(ROOT, "oracle", "_ref", f"librtgref_S{S}.so")
+    port = os.path.join(ROOT, "oracle", "build", "librtg_oracle.so")
+    kind = "reference" if os.path.exists(ref) else "port"
+    L = ctypes.CDLL(ref if kind == "reference" else port)
+    P = lambda a: ctypes.c_void_p(a.ctypes.data) if a.size else None  # noqa: E731
+
+    def run(rows):
+        rows = np.asarray(rows, np.uint32)
+        out = np.zeros((len(rows), W, 3), np.float32)
+        t0 = time.perf_counter()
+        if kind == "reference":
+            L.ref_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
+                              ctypes.c_float(3.0), P(rows), len(rows), P(out), 1)
+        else:
+            L.oracle_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
+                                 ctypes.c_float(3.0), S, P(rows), len(rows), P(out), 1, None)
+        return time.perf_counter() - t0, out
+
+    # calibrate on a 1/64 stride, then pick the stride that fits the budget
+    t_cal, _ = run(range(0, H, 64))
+    est_full = t_cal * 64
+    stride = max(1, int(np.ceil(est_full / budget_s)))
+    rows = list(range(0, H, stride))
+    t, out = run(rows)
+    px = len(rows) * W
+    return {"value": round(px / t / 1e6, 5), "unit": "Mpixels/s", "cores": 1, "kind": kind,
+            "sample": f"{name} rows 0,{stride},{2 * stride},... ({len(rows)} of {H} rows, "
+                      f"{px} px, {t:.1f} s, 1 thread)",
+            "frame_s_extrapolated": round(t * H / len(rows), 1)}, rows, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H, n, m, depth = CONFIGS[args.config]
+    S = depth + 1
+    B = args.row_block
+    sph, lg = R.generate_scene(n, m, 42)
+    ctx = R.Context(local)
+    ctx.set_scene(sph, lg)
+    if args.variant:
+        ctx.set_variant(args.variant)
+
+    Rmax = rdist.padded_rows(H, B, world)
+    my_rows = R.shard_rows(H, B, rank, world)
+    shard = torch.zeros((Rmax, W, 3), dtype=torch.float32, device="cuda")
+    gathered = (torch.empty((world, Rmax, W, 3), dtype=torch.float32, device="cuda")
+                if (world > 1 and rank == 0) else None)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(args.steps)]
+
+    frame = None
+
+    def step(i=None):
+        nonlocal frame
+        if i is not None:
+            ev_k[i][0].record(stream)
+        ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, shard=rank,
+                          n_shards=world, stream=sptr)
+        if i is not None:
+            ev_k[i][1].record(stream)
+        if world > 1:
+            dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                frame = rdist.assemble(gathered, H, B).contiguous()
+        else:
+            frame = shard
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_k]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_max_ms = float(t[0]), float(t[1])
+    else:
+        kern_max_ms = kern_ms
+
+    ms_per_step = elapsed / args.steps * 1e3
+    mpx = W * H / (elapsed / args.steps) / 1e6
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    # ---------------- parity of the produced frame vs the reference goldens
+    golden = json.load(open(GOLDEN)) if os.path.exists(GOLDEN) else {"configs": {}}
+    g = golden["configs"].get(args.config, {})
+    fb = frame.cpu().numpy()
+    parity = {"reference": "tests/golden (reference raytracer.h output)"}
+    if "fb_md5" in g:
+        got = canon_md5(fb)
+        parity["fb_md5_match"] = got == g["fb_md5"]
+        mx = R.max_colour_value(fb)
+        ppm = R.ppm_file_bytes(fb, mx)
+        parity["ppm_md5_match"] = hashlib.md5(ppm).hexdigest() == g["ppm_md5"]
+        parity["max_colour_match"] = int(np.float32(mx).view(np.uint32)) == g["max_colour_bits"]
+    # max-abs-diff vs the reference CPU path on golden rows (and CPU sample below)
+    rows_file = os.path.join(ROOT, "tests", "golden", f"{args.config}.rows.f32")
+    diffs = []
+    if "rows" in g and os.path.exists(rows_file):
+        rows = g["rows"]["rows"]
+        want = np.fromfile(rows_file, np.float32).reshape(len(rows), W, 3)
+        diffs.append((fb[rows], want))
+
+    # ---------------- CPU baseline (rank 0, N = 1 only)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu, crow, cout = cpu_baseline(args.config, sph, lg, W, H, S, args.cpu_budget)
+        diffs.append((fb[crow], cout))
+    if diffs:
+        a = np.concatenate([d[0].reshape(-1) for d in diffs])
+        b = np.concatenate([d[1].reshape(-1) for d in diffs])
+        nan_a, nan_b = np.isnan(a), np.isnan(b)
+        ok = ~(nan_a | nan_b)
+        parity["max_abs_diff_float"] = float(np.max(np.abs(a[ok] - b[ok]))) if ok.any() else 0.0
+        parity["nan_positions_match"] = bool((nan_a == nan_b).all())
+        parity["values_compared"] = int(a.size)
+        # PPM bytes of those pixels under the frame's max colour
+        mx = R.max_colour_value(fb)
+        pa, pb = R.ppm_bytes(a.reshape(-1, 3), mx), R.ppm_bytes(b.reshape(-1, 3), mx)
+        parity["ppm_max_abs_diff"] = int(np.max(np.abs(pa.astype(int) - pb.astype(int))))
+
+    # ---------------- roofline (rank-0 launch)
+    tests = g.get("ray_sphere_tests")
+    roof = None
+    if tests:
+        frac_rows = my_rows / H  # exact for N = 1; row-proportional estimate for N > 1
+        flops = tests * FLOPS_PER_TEST * frac_rows
+        ach = flops / (kern_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "TFLOP/s", "frac": round(ach / VALU_PEAK_TOPS, 4), "traffic": None,
+                "work": f"{tests} reference ray-sphere tests x {FLOPS_PER_TEST} FP32 ops "
+                        f"x {frac_rows:.4f} of rows, / mean kernel time {kern_ms:.3f} ms (HIP events "
+                        f"on the launch stream)",
+                "hbm": {"achieved_GBs": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9, 2),
+                        "peak_GBs": HBM_PEAK_GBS,
+                        "frac": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+                        "algorithmic_bytes": my_rows * W * 12}}
+        tr = os.environ.get("RTG_PMC_TRAFFIC_BYTES")  # filled from profiles/ when known
+        if tr:
+            roof["traffic"] = int(tr)
+
+    out = {
+        "metric": METRIC, "value": round(mpx, 2), "unit": "Mpixels/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: seeded scene generator (SURVEY.md §8d, seed 42), resident in HBM",
+        "config": {"workload": f"{args.config}: {W}x{H}, {n} spheres, {m} lights, depth {depth} "
+                               f"(RTSTACK_MAXSIZE {S}), 3x3 supersampling",
+                   "width": W, "height": H, "spheres": n, "lights": m, "depth": depth,
+                   "alias_factor": 3, "row_block": B, "variant": args.variant,
+                   "parallelism": f"row-cyclic x{world}" + (" + RCCL gather" if world > 1 else "")},
+        "mrays_per_s": round(mpx * 9, 1),
+        "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
+        "roofline": roof, "cpu_baseline": cpu,
+        "gpu_vs_cpu": round(mpx / cpu["value"], 1) if cpu else None,
+        "parity": parity,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * rtg.h — C ABI of the MI355X-native raytracer-gamma hot path (librtg.so).
+ *
+ * This header is the drop-in boundary that replaces the reference's OpenCL
+ * enqueue of the per-pixel kernel:
+ *
+ *   reference (snowzurfer/raytracer-gamma)            replaced by
+ *   ------------------------------------------------  ------------------------------
+ *   clCreateBuffer/clEnqueueWriteBuffer scene          rtg_render (one-shot) or
+ *     main.cpp:277-294                                 rtg_context_set_scene
+ *   clSetKernelArg x11, clEnqueueNDRangeKernel,        rtg_render / rtg_render_device /
+ *     clFinish  main.cpp:339-363                       rtg_render_rows[_device]
+ *     (kernel raytrace_kernel.cl:870-881)
+ *   clEnqueueReadBuffer  main.cpp:460                  rtg_render (dstHost) or the
+ *                                                      caller's copy of dstDevice
+ *   maxColourValuePixelBuffer  algebra.h:68-91         rtg_max_colour (host) /
+ *                                                      rtg_max_colour_device
+ *   savePPM  main.cpp:43-91                            rtg_save_ppm / rtg_ppm_bytes
+ *   rayTrace(...)  raytracer.h:410-636 (CPU entry)     (inside the HIP kernel)
+ *   checkError -> exit(EXIT_FAILURE)  err_code.h:143   negative return + rtg_last_error
+ *   output_device_info  device_info.cpp:30             rtg_device_info
+ *   parseArguments --list/--device  device_picker.h:70 rtg_device_count / device index args
+ *
+ * Scene records are byte-identical to the reference structs (static_asserts in
+ * the implementation): a `struct Sphere*` / `struct Light*` / `Vec*` from the
+ * reference host can be passed by a plain pointer cast.
+ *
+ * Semantics: the output is the framebuffer the reference CPU path
+ * (raytracer.h, main.cpp:404-453) produces, bit for bit (NaNs are written as
+ * the x86 default NaN 0xFFC00000 that path produces).  `stackSize` is the
+ * reference's RTSTACK_MAXSIZE (raytraceStack.h:10; 6 as shipped) = depth + 1.
+ *
+ * All calls are blocking unless they take a `stream`; no call exits the
+ * process.  Not re-entrant per context.
+ */
+#ifndef RTG_H
+#define RTG_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTG_ABI_VERSION 1
+#define RTG_MAX_STACK 16 /* largest supported RTSTACK_MAXSIZE */
+
+/* vec.h:27-29 */
+typedef struct rtg_vec { float x, y, z; } rtg_vec;
+/* material.h:8-14 */
+typedef struct rtg_material {
+  rtg_vec matteColour;
+  rtg_vec glossColour;
+  float opacity;
+  float refractiveIndex;
+} rtg_material;
+/* sphere.h:9-14 */
+typedef struct rtg_sphere {
+  rtg_vec pos;
+  float radius;
+  rtg_material material;
+} rtg_sphere;
+/* raytracer.h:20-25 */
+typedef struct rtg_light { rtg_vec pos; rtg_vec col; } rtg_light;
+
+/* Error codes (err_code.h:143-155 printed-and-exited; here they are returned). */
+#define RTG_OK 0
+#define RTG_ERR_INVALID (-1)   /* bad argument */
+#define RTG_ERR_HIP (-2)       /* HIP runtime error; see rtg_last_error() */
+#define RTG_ERR_NOMEM (-3)
+#define RTG_ERR_NODEVICE (-4)
+#define RTG_ERR_IO (-5)
+
+/* Thread-local message for the last failing call ("" if none). */
+const char* rtg_last_error(void);
+int rtg_abi_version(void);
+
+/* ---- device selection (device_picker.h:70-119, device_info.cpp:30-125) ---- */
+int rtg_device_count(int* count);
+/* Writes a one-line description ("name, CUs, clock, memory") into buf. */
+int rtg_device_info(int device, char* buf, size_t buflen);
+
+/* ---- one-shot drop-in for main.cpp:277-468 ----
+ * Uploads the scene, renders the whole W x H frame on `device`, downloads
+ * W*H rtg_vec into dstHost.  aliasFactor: the reference's kAliasFactor (3.f =
+ * 3x3 supersampling); zoom: kZoom (-4.f). */
+int rtg_render(int device, const rtg_sphere* spheres, unsigned sphNum,
+               const rtg_light* lights, unsigned lgtNum, unsigned width,
+               unsigned height, float zoom, float aliasFactor, int stackSize,
+               rtg_vec* dstHost);
+
+/* ---- persistent context: scene resident in HBM, caller-owned streams ---- */
+typedef struct rtg_context rtg_context;
+int rtg_context_create(int device, rtg_context** out);
+int rtg_context_destroy(rtg_context* ctx);
+/* Copies the scene into device memory (kept until the next call / destroy). */
+int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned sphNum,
+                          const rtg_light* lights, unsigned lgtNum);
+
+/* Row sharding.  Rows are grouped in blocks of `rowBlock` rows; block b belongs
+ * to shard (b % nShards) (row-cyclic).  A shard's rows are
+ * packed in increasing row order.  nShards == 1 gives the whole frame in
+ * row-major order.  Returns the number of rows of `shard` in *rows. */
+int rtg_shard_rows(unsigned height, unsigned rowBlock, unsigned shard, unsigned nShards,
+                   unsigned* rows);
+/* Global row index of local row `localRow` of `shard`. */
+unsigned rtg_shard_global_row(unsigned localRow, unsigned rowBlock, unsigned shard,
+                              unsigned nShards);
+
+/* Asynchronous render of shard `shard` of a W x H frame into device memory
+ * dstDevice (rtg_shard_rows(...) * W rtg_vec) on `stream` (a hipStream_t, or
+ * NULL for the null stream).  The camera uses global row indices, so the
+ * shard's pixels are bit-identical to the same pixels of a 1-shard render. */
+int rtg_render_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
+                      float aliasFactor, int stackSize, unsigned rowBlock, unsigned shard,
+                      unsigned nShards, rtg_vec* dstDevice, void* stream);
+
+/* Render an explicit list of global rows (each < height) into dstDevice
+ * (nRows * width rtg_vec, in list order); rowsDevice is device memory. */
+int rtg_render_rows_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
+                           float aliasFactor, int stackSize, const unsigned* rowsDevice,
+                           unsigned nRows, rtg_vec* dstDevice, void* stream);
+/* One-shot host version of the above (rows and dstHost in host memory). */
+int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
+                    const rtg_light* lights, unsigned lgtNum, unsigned width, unsigned height,
+                    float zoom, float aliasFactor, int stackSize, const unsigned* rows,
+                    unsigned nRows, rtg_vec* dstHost);
+
+/* Launch-configuration knobs (performance only; results never change). */
+typedef struct rtg_launch_opts {
+  int variant;        /* 0 = default kernel; other values select A/B variants */
+  int reserved[7];
+} rtg_launch_opts;
+int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts);
+
+/* ---- output side ---- */
+/* algebra.h:68-91 on the host. */
+float rtg_max_colour(const rtg_vec* pixels, size_t n);
+/* Same reduction on the device into *maxDevice (one float), on `stream`. */
+int rtg_max_colour_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n,
+                          float* maxDevice, void* stream);
+/* main.cpp:66-81: 3 bytes per pixel, (unsigned char)(min(1,c)*255/max) with the
+ * x86 truncating conversion (low byte of a 32-bit cvttss2si). */
+void rtg_ppm_bytes(const rtg_vec* pixels, size_t n, float maxColourVal,
+                   unsigned char* out);
+/* Device version: reads *maxDevice, writes n*3 bytes to outDevice. */
+int rtg_ppm_bytes_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n,
+                         const float* maxDevice, unsigned char* outDevice, void* stream);
+/* main.cpp:43-91: binary P6 writer. */
+int rtg_save_ppm(const rtg_vec* pixels, const char* filename, int width, int height,
+                 float maxColourVal);
+
+/* ---- scene construction helpers (main.cpp:53-74, 113-168) ---- */
+/* setMatOpacity + setMatteGlossBalance + setMatRefractivityIndex. */
+void rtg_make_material(float opacity, float glossFactor, const rtg_vec* matte,
+                       const rtg_vec* gloss, float refractiveIndex, rtg_material* out);
+/* The reference's hard-coded 3-sphere / 2-light scene (main.cpp:104-168) when
+ * sphNum<=3 && lgtNum<=2, extended by the seeded generator of SURVEY.md §8d.
+ * seed 42 is the benchmark scene. */
+int rtg_scene_generate(unsigned long long seed, unsigned sphNum, unsigned lgtNum,
+                       rtg_sphere* spheres, rtg_light* lights);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTG_H */

@@ -1,0 +1,505 @@
+// rtg_kernel.hip — CDNA4 (gfx950) kernels and the device half of the C ABI.
+//
+// Replaces the OpenCL kernel `raytrace` (raytrace_kernel.cl:870-973) and its
+// host orchestration (main.cpp:277-363, 456-468), computing the reference CPU
+// path's framebuffer (raytracer.h) bit for bit; see rtg_trace.h for the
+// traversal and DESIGN.md for the layout and roofline.
+//
+// Launch geometry: one work-item per pixel; a 256-thread workgroup covers a
+// 16x16 pixel tile and each 64-lane wave an 8x8 sub-tile, so the rays of a
+// wave are spatially coherent and take similar paths through the Whitted tree.
+// The sphere loop index is wave-uniform, so sphere records are read with
+// scalar loads into SGPRs (no VGPRs, no LDS traffic); per-lane material
+// lookups (the hit sphere / refractive medium) come from an LDS copy of the
+// material table staged once per workgroup.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <type_traits>
+#include <vector>
+
+#include "rtg.h"
+#include "rtg_internal.h"
+#include "rtg_trace.h"
+#include "rtg_scene_pack.h"
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      rtg_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                     \
+      return RTG_ERR_HIP;                                                          \
+    }                                                                              \
+  } while (0)
+
+namespace rtg {
+
+constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
+// Materials staged in LDS when the table fits (n+1 records of 32 B).
+constexpr unsigned kLdsMatMax = 1024 + 1;
+
+// Device scene: geometry SoA-ish float4 {x, y, z, r*r}, (r + 1e-6f)^2, the
+// material table (n+1 x 8 floats; [n] = background), lights (m x 6 floats).
+// Read-only scene arrays are accessed through the constant address space
+// (addrspace 4): with a wave-uniform index the loads become s_load into SGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTG_CONST __attribute__((address_space(4)))
+#else
+#define RTG_CONST
+#endif
+typedef const RTG_CONST float* cfloat_p;
+
+template <class MatPtr>
+struct DevScene {
+  cfloat_p geom;      // n x {x, y, z, r*r}
+  cfloat_p crad2;
+  MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)
+  cfloat_p lights;
+  unsigned n, m;
+
+  __device__ __forceinline__ V3 sphere(unsigned i, float& r2) const {
+    cfloat_p g = geom + 4 * i;
+    r2 = g[3];
+    return v3(g[0], g[1], g[2]);
+  }
+  __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
+  __device__ __forceinline__ Mat mat(int i) const {
+    const auto p = mats + 8 * i;
+    Mat r;
+    r.matte = v3(p[0], p[1], p[2]);
+    r.gloss = v3(p[3], p[4], p[5]);
+    r.opacity = p[6];
+    r.refr = p[7];
+    return r;
+  }
+  __device__ __forceinline__ float refr(int i) const { return mats[8 * i + 7]; }
+  __device__ __forceinline__ void light(unsigned l, V3& pos, V3& col) const {
+    cfloat_p p = lights + 6 * l;
+    pos = v3(p[0], p[1], p[2]);
+    col = v3(p[3], p[4], p[5]);
+  }
+};
+
+struct KernelArgs {
+  const float4* geom;
+  const float* crad2;
+  const float* mats;
+  const float* lights;
+  unsigned n, m;
+  Camera cam;
+  unsigned W, rowsLocal, rowBlock, shard, nShards;
+  const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
+  float* dst;
+};
+
+__device__ __forceinline__ float canon_nan(float v) {
+  // x86 default NaN, what the reference CPU path writes (see rtg.h).
+  return (v != v) ? __uint_as_float(0xFFC00000u) : v;
+}
+
+template <int S, bool kLdsMats>
+__global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
+  extern __shared__ float lmats[];  // (n+1)*8 floats when kLdsMats
+  typedef typename std::conditional<kLdsMats, const float*, cfloat_p>::type MatPtr;
+  DevScene<MatPtr> sc;
+  if constexpr (kLdsMats) {
+    const unsigned nm = (a.n + 1) * 8;
+    for (unsigned i = threadIdx.x; i < nm; i += kBlock) lmats[i] = a.mats[i];
+    __syncthreads();
+    sc.mats = lmats;
+  } else {
+    sc.mats = (cfloat_p)a.mats;
+  }
+  sc.geom = (cfloat_p)a.geom;
+  sc.crad2 = (cfloat_p)a.crad2;
+  sc.lights = (cfloat_p)a.lights;
+  sc.n = a.n;
+  sc.m = a.m;
+
+  const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const unsigned x = blockIdx.x * kTileW + (wave & 1u) * 8u + (lane & 7u);
+  const unsigned lr = blockIdx.y * kTileH + (wave >> 1) * 8u + (lane >> 3);
+  if (x >= a.W || lr >= a.rowsLocal) return;
+  const unsigned gy =
+      a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
+  const V3 pix = shade_pixel<S>(sc, a.cam, x, gy);
+  float* o = a.dst + ((size_t)lr * a.W + x) * 3;
+  o[0] = canon_nan(pix.x);
+  o[1] = canon_nan(pix.y);
+  o[2] = canon_nan(pix.z);
+}
+
+// algebra.h:68-91 on the device: values are compared as floats (NaN never
+// wins), the running max starts at +0 so only positive values can win, and a
+// non-negative float orders like its bit pattern, so an integer atomicMax on
+// the bits reduces across workgroups.
+__global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ c, size_t nval,
+                                                  unsigned* __restrict__ out) {
+  float mx = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nval;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const float v = c[i];
+    if (v > mx) mx = v;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const float o = __shfl_xor(mx, off);
+    if (o > mx) mx = o;
+  }
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (part[w] > mx) mx = part[w];
+    atomicMax(out, __float_as_uint(mx));
+  }
+}
+
+__global__ void max_finish_kernel(unsigned* m) {
+  if (__uint_as_float(*m) == 0.f) *m = __float_as_uint(1.f);
+}
+
+__global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, size_t nval,
+                                                  const float* __restrict__ mx,
+                                                  unsigned char* __restrict__ out) {
+  const float m = *mx;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nval;
+       i += (size_t)gridDim.x * blockDim.x)
+    out[i] = ppm_byte(c[i], m);
+}
+
+typedef void (*TraceFn)(const KernelArgs);
+template <int S>
+static TraceFn trace_fn(bool lds) { return lds ? trace_kernel<S, true> : trace_kernel<S, false>; }
+
+static TraceFn pick_trace(int S, bool lds) {
+  switch (S) {
+#define RTG_CASE(k) case k: return trace_fn<k>(lds);
+    RTG_CASE(1) RTG_CASE(2) RTG_CASE(3) RTG_CASE(4) RTG_CASE(5) RTG_CASE(6) RTG_CASE(7)
+    RTG_CASE(8) RTG_CASE(9) RTG_CASE(10) RTG_CASE(11) RTG_CASE(12) RTG_CASE(13)
+    RTG_CASE(14) RTG_CASE(15) RTG_CASE(16)
+#undef RTG_CASE
+    default: return nullptr;
+  }
+}
+
+}  // namespace rtg
+
+struct rtg_context {
+  int device = 0;
+  unsigned n = 0, m = 0;
+  float4* geom = nullptr;
+  float* crad2 = nullptr;
+  float* mats = nullptr;
+  float* lights = nullptr;
+  unsigned* maxScratch = nullptr;
+  rtg_launch_opts opts{};
+  bool hasScene = false;
+};
+
+using namespace rtg;
+
+static void free_scene(rtg_context* c) {
+  (void)hipFree(c->geom);
+  (void)hipFree(c->crad2);
+  (void)hipFree(c->mats);
+  (void)hipFree(c->lights);
+  c->geom = nullptr;
+  c->crad2 = nullptr;
+  c->mats = nullptr;
+  c->lights = nullptr;
+  c->hasScene = false;
+}
+
+extern "C" {
+
+int rtg_device_count(int* count) {
+  rtg_clear_error();
+  if (!count) return RTG_ERR_INVALID;
+  HIP_TRY(hipGetDeviceCount(count));
+  return RTG_OK;
+}
+
+int rtg_device_info(int device, char* buf, size_t buflen) {
+  rtg_clear_error();
+  if (!buf || buflen == 0) return RTG_ERR_INVALID;
+  hipDeviceProp_t p;
+  HIP_TRY(hipGetDeviceProperties(&p, device));
+  snprintf(buf, buflen, "%s (%s), %d CUs, %d MHz, %.1f GiB, LDS/block %zu KiB", p.name,
+           p.gcnArchName, p.multiProcessorCount, p.clockRate / 1000,
+           (double)p.totalGlobalMem / (1024.0 * 1024.0 * 1024.0),
+           (size_t)p.sharedMemPerBlock / 1024);
+  return RTG_OK;
+}
+
+int rtg_context_create(int device, rtg_context** out) {
+  rtg_clear_error();
+  if (!out) return RTG_ERR_INVALID;
+  *out = nullptr;
+  int cnt = 0;
+  HIP_TRY(hipGetDeviceCount(&cnt));
+  if (device < 0 || device >= cnt) {
+    rtg_set_error("device %d not present (%d devices)", device, cnt);
+    return RTG_ERR_NODEVICE;
+  }
+  HIP_TRY(hipSetDevice(device));
+  rtg_context* c = new rtg_context();
+  c->device = device;
+  if (hipMalloc(&c->maxScratch, 4) != hipSuccess) {
+    delete c;
+    rtg_set_error("hipMalloc failed");
+    return RTG_ERR_NOMEM;
+  }
+  *out = c;
+  return RTG_OK;
+}
+
+int rtg_context_destroy(rtg_context* ctx) {
+  rtg_clear_error();
+  if (!ctx) return RTG_OK;
+  (void)hipSetDevice(ctx->device);
+  free_scene(ctx);
+  (void)hipFree(ctx->maxScratch);
+  delete ctx;
+  return RTG_OK;
+}
+
+int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts) {
+  rtg_clear_error();
+  if (!ctx || !opts) return RTG_ERR_INVALID;
+  ctx->opts = *opts;
+  return RTG_OK;
+}
+
+int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned sphNum,
+                          const rtg_light* lights, unsigned lgtNum) {
+  rtg_clear_error();
+  if (!ctx || (sphNum && !spheres) || (lgtNum && !lights)) {
+    rtg_set_error("rtg_context_set_scene: invalid arguments");
+    return RTG_ERR_INVALID;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  free_scene(ctx);
+  PackedScene ps;
+  pack_scene(spheres, sphNum, lights, lgtNum, &ps);
+  std::vector<float4> geom(ps.geom.size() / 4);
+  memcpy(geom.data(), ps.geom.data(), ps.geom.size() * sizeof(float));
+  const std::vector<float>& crad2 = ps.crad2;
+  const std::vector<float>& mats = ps.mats;
+  const std::vector<float>& lg = ps.lights;
+  if (hipMalloc(&ctx->geom, geom.size() * sizeof(float4)) != hipSuccess ||
+      hipMalloc(&ctx->crad2, crad2.size() * sizeof(float)) != hipSuccess ||
+      hipMalloc(&ctx->mats, mats.size() * sizeof(float)) != hipSuccess ||
+      hipMalloc(&ctx->lights, lg.size() * sizeof(float)) != hipSuccess) {
+    free_scene(ctx);
+    rtg_set_error("hipMalloc failed for scene");
+    return RTG_ERR_NOMEM;
+  }
+  HIP_TRY(hipMemcpy(ctx->geom, geom.data(), geom.size() * sizeof(float4),
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->crad2, crad2.data(), crad2.size() * sizeof(float),
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->mats, mats.data(), mats.size() * sizeof(float),
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(ctx->lights, lg.data(), lg.size() * sizeof(float), hipMemcpyHostToDevice));
+  ctx->n = sphNum;
+  ctx->m = lgtNum;
+  ctx->hasScene = true;
+  return RTG_OK;
+}
+
+static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float zoom,
+                        float aliasFactor, int stackSize, unsigned rowBlock, unsigned shard,
+                        unsigned nShards, const unsigned* rowList, unsigned nRowList,
+                        rtg_vec* dstDevice, void* stream) {
+  if (!ctx || !ctx->hasScene) {
+    rtg_set_error("render: no context/scene");
+    return RTG_ERR_INVALID;
+  }
+  const bool ldsMats = ctx->n + 1 <= kLdsMatMax;
+  TraceFn fn = pick_trace(stackSize, ldsMats);
+  if (!fn) {
+    rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
+    return RTG_ERR_INVALID;
+  }
+  KernelArgs a;
+  int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
+  if (rc) return rc;
+  unsigned rows;
+  if (rowList) {
+    rows = nRowList;
+  } else {
+    if (rowBlock == 0 || nShards == 0 || shard >= nShards) {
+      rtg_set_error("render: bad sharding %u/%u block %u", shard, nShards, rowBlock);
+      return RTG_ERR_INVALID;
+    }
+    rows = shard_row_count(height, rowBlock, shard, nShards);
+  }
+  if (rows == 0) return RTG_OK;
+  if (!dstDevice) {
+    rtg_set_error("render: null destination");
+    return RTG_ERR_INVALID;
+  }
+  a.geom = ctx->geom;
+  a.crad2 = ctx->crad2;
+  a.mats = ctx->mats;
+  a.lights = ctx->lights;
+  a.n = ctx->n;
+  a.m = ctx->m;
+  a.W = width;
+  a.rowsLocal = rows;
+  a.rowBlock = rowBlock ? rowBlock : 1;
+  a.shard = shard;
+  a.nShards = nShards ? nShards : 1;
+  a.rowList = rowList;
+  a.dst = reinterpret_cast<float*>(dstDevice);
+  HIP_TRY(hipSetDevice(ctx->device));
+  dim3 grid((width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
+  const size_t lds = ldsMats ? (size_t)(ctx->n + 1) * 8 * sizeof(float) : 0;
+  hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, (hipStream_t)stream, a);
+  HIP_TRY(hipGetLastError());
+  return RTG_OK;
+}
+
+int rtg_render_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
+                      float aliasFactor, int stackSize, unsigned rowBlock, unsigned shard,
+                      unsigned nShards, rtg_vec* dstDevice, void* stream) {
+  rtg_clear_error();
+  return launch_trace(ctx, width, height, zoom, aliasFactor, stackSize, rowBlock, shard,
+                      nShards, nullptr, 0, dstDevice, stream);
+}
+
+int rtg_render_rows_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
+                           float aliasFactor, int stackSize, const unsigned* rowsDevice,
+                           unsigned nRows, rtg_vec* dstDevice, void* stream) {
+  rtg_clear_error();
+  if (nRows && !rowsDevice) {
+    rtg_set_error("rtg_render_rows_device: null row list");
+    return RTG_ERR_INVALID;
+  }
+  if (nRows == 0) return RTG_OK;
+  return launch_trace(ctx, width, height, zoom, aliasFactor, stackSize, 1, 0, 1, rowsDevice,
+                      nRows, dstDevice, stream);
+}
+
+int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
+                    const rtg_light* lights, unsigned lgtNum, unsigned width, unsigned height,
+                    float zoom, float aliasFactor, int stackSize, const unsigned* rows,
+                    unsigned nRows, rtg_vec* dstHost) {
+  rtg_clear_error();
+  if (nRows && (!rows || !dstHost)) {
+    rtg_set_error("rtg_render_rows: null argument");
+    return RTG_ERR_INVALID;
+  }
+  for (unsigned k = 0; k < nRows; ++k)
+    if (rows[k] >= height) {
+      rtg_set_error("rtg_render_rows: row %u >= height %u", rows[k], height);
+      return RTG_ERR_INVALID;
+    }
+  if (nRows == 0) return RTG_OK;
+  rtg_context* ctx = nullptr;
+  int rc = rtg_context_create(device, &ctx);
+  if (rc) return rc;
+  rtg_vec* d = nullptr;
+  unsigned* drows = nullptr;
+  const size_t bytes = (size_t)width * nRows * sizeof(rtg_vec);
+  rc = rtg_context_set_scene(ctx, spheres, sphNum, lights, lgtNum);
+  if (!rc && (hipMalloc(&d, bytes) != hipSuccess ||
+              hipMalloc(&drows, nRows * sizeof(unsigned)) != hipSuccess)) {
+    rtg_set_error("hipMalloc failed");
+    rc = RTG_ERR_NOMEM;
+  }
+  if (!rc && hipMemcpy(drows, rows, nRows * sizeof(unsigned), hipMemcpyHostToDevice) !=
+                 hipSuccess) {
+    rtg_set_error("row list upload failed");
+    rc = RTG_ERR_HIP;
+  }
+  if (!rc)
+    rc = rtg_render_rows_device(ctx, width, height, zoom, aliasFactor, stackSize, drows, nRows,
+                                d, nullptr);
+  if (!rc) {
+    hipError_t e = hipMemcpy(dstHost, d, bytes, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      rtg_set_error("kernel/readback failed: %s", hipGetErrorString(e));
+      rc = RTG_ERR_HIP;
+    }
+  }
+  (void)hipFree(d);
+  (void)hipFree(drows);
+  rtg_context_destroy(ctx);
+  return rc;
+}
+
+int rtg_max_colour_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n,
+                          float* maxDevice, void* stream) {
+  rtg_clear_error();
+  if (!ctx || !maxDevice || (n && !pixelsDevice)) return RTG_ERR_INVALID;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemsetAsync(maxDevice, 0, sizeof(float), s));
+  if (n) {
+    const size_t nval = n * 3;
+    size_t blocks = (nval + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(max_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const float*)pixelsDevice, nval, (unsigned*)maxDevice);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(max_finish_kernel, dim3(1), dim3(1), 0, s, (unsigned*)maxDevice);
+  HIP_TRY(hipGetLastError());
+  return RTG_OK;
+}
+
+int rtg_ppm_bytes_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n,
+                         const float* maxDevice, unsigned char* outDevice, void* stream) {
+  rtg_clear_error();
+  if (!ctx || !maxDevice || (n && (!pixelsDevice || !outDevice))) return RTG_ERR_INVALID;
+  if (n == 0) return RTG_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const size_t nval = n * 3;
+  size_t blocks = (nval + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(ppm_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)pixelsDevice, nval, maxDevice, outDevice);
+  HIP_TRY(hipGetLastError());
+  return RTG_OK;
+}
+
+int rtg_render(int device, const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
+               unsigned lgtNum, unsigned width, unsigned height, float zoom, float aliasFactor,
+               int stackSize, rtg_vec* dstHost) {
+  rtg_clear_error();
+  if (!dstHost) {
+    rtg_set_error("rtg_render: null destination");
+    return RTG_ERR_INVALID;
+  }
+  rtg_context* ctx = nullptr;
+  int rc = rtg_context_create(device, &ctx);
+  if (rc) return rc;
+  rtg_vec* d = nullptr;
+  const size_t bytes = (size_t)width * height * sizeof(rtg_vec);
+  rc = rtg_context_set_scene(ctx, spheres, sphNum, lights, lgtNum);
+  if (!rc && hipMalloc(&d, bytes ? bytes : 4) != hipSuccess) {
+    rtg_set_error("hipMalloc(%zu) failed", bytes);
+    rc = RTG_ERR_NOMEM;
+  }
+  if (!rc)
+    rc = rtg_render_device(ctx, width, height, zoom, aliasFactor, stackSize, 16, 0, 1, d,
+                           nullptr);
+  if (!rc) {
+    hipError_t e = hipMemcpy(dstHost, d, bytes, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      rtg_set_error("kernel/readback failed: %s", hipGetErrorString(e));
+      rc = RTG_ERR_HIP;
+    }
+  }
+  (void)hipFree(d);
+  rtg_context_destroy(ctx);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,359 @@
+// rtg_trace.h — per-pixel Whitted traversal of raytracer-gamma, written for
+// the CDNA4 kernel in rtg_kernel.hip.
+//
+// It computes exactly what the reference CPU path computes (raytracer.h +
+// raytraceStack.h + main.cpp:411-452), bit for bit, but is restructured for a
+// 64-lane wave:
+//
+//  * The reference's 168-byte snapshot stack (raytraceStack.h:13-35) becomes a
+//    stack of 52-byte frames, one per ANCESTOR level 0..S-2.  A frame carries
+//    the node colour, the pre-computed reflection child ray (the stage-1 work
+//    of raytracer.h:552-618 depends only on stage-0 values, so it is done
+//    before descending; same operations, same order) and the refractive
+//    material index.
+//  * The shared `colourSum` return register (raytracer.h:425) is kept as
+//    `ret`.  Its "stale" value — read when a child hits with insignificant
+//    intensity (raytracer.h:460 false branch) or when a child push was dropped
+//    by a full stack (raytraceStack.h:52-58) — is always the parent's colour
+//    at push time, which the code sets explicitly before every descent.
+//  * Nodes at the last level (S-1) never get children: their refraction and
+//    reflection children are dropped by the full stack, which the reference
+//    turns into colour doubling (colour+colour, then again if the reflection
+//    was significant).  The leaf path computes that directly, without a frame
+//    and without the child rays.
+//  * Shadow rays (raytracer.h:272-309) stop at the first blocker: blocked iff
+//    some sphere has a valid root t < 1000 with |t*D|^2 < gap.  This is exact
+//    because |fl(t*D)|^2 is monotone in t under round-to-nearest, so the
+//    closest hit blocks whenever any hit does.  A light with incidence <= 0
+//    (raytracer.h:349) contributes nothing, so its shadow ray is skipped.
+//  * All per-sphere constants that the reference recomputes (r*r,
+//    (r+1e-6f)^2) are precomputed on the host with the same float operation.
+//
+// Arithmetic follows the reference's operation order exactly; the file must
+// be compiled with -ffp-contract=off and without fast-math (correctly rounded
+// f32 division and sqrt are the HIP defaults and are checked by the GPU tests).
+#pragma once
+
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RTG_HD __host__ __device__ __forceinline__
+#else
+#define RTG_HD inline
+#endif
+
+namespace rtg {
+
+struct V3 { float x, y, z; };
+
+RTG_HD V3 v3(float a, float b, float c) { V3 r; r.x = a; r.y = b; r.z = c; return r; }
+// vec.h:34-41, operand order preserved.
+RTG_HD V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RTG_HD V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RTG_HD V3 vmul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RTG_HD V3 vsmul(float k, V3 b) { return v3(k * b.x, k * b.y, k * b.z); }
+RTG_HD float vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RTG_HD float rtg_sqrtf(float x) { return sqrtf(x); }
+RTG_HD V3 vnorm(V3 v) { float l = 1.f / rtg_sqrtf(vdot(v, v)); return vsmul(l, v); }
+// raytracer.h:235-241
+RTG_HD bool significant(V3 c) { return (c.x >= 0.001f) || (c.y >= 0.001f) || (c.z >= 0.001f); }
+
+// Camera constants of main.cpp:384-402, computed once on the host.
+struct Camera {
+  float xs, ys, asp, st, inv, halfW, halfH, zoom;
+  int nAA;  // iterations of `for (int i = 0; i < aliasFactor; ++i)`
+};
+
+// Material record (material.h:8-14) as 8 floats; index n is the background
+// material {0,0,0, 0,0,0, opacity 0, n 1.0} (raytracer.h:694-697).
+struct Mat { V3 matte, gloss; float opacity, refr; };
+
+// One ancestor frame.
+struct Frame {
+  V3 colour;
+  V3 ro, rd, rI;   // pre-computed reflection child ray (valid if sig)
+  int rm;          // refractive material index of this node (stage-1/2 use)
+  int flags;       // bit0: stage==2, bit1: reflection child significant
+};
+
+// ---------------------------------------------------------------------------
+// Per-sphere ray test, raytracer.h:81-141.  Returns the smallest root in
+// (1e-5, 10000) or 10000 when none (`res` tells).  a4 = 4.0f*a, den = 2.0f*a.
+RTG_HD float ray_sphere(V3 o, V3 d, V3 c, float r2, float a4, float den, bool& res) {
+  V3 disp = vsub(o, c);
+  const float b = 2.0f * vdot(d, disp);
+  const float cc = vdot(disp, disp) - r2;
+  const float radicand = (b * b) - (a4 * cc);
+  float sm = 10000.f;
+  res = false;
+  if (radicand >= 0.0f) {
+    const float root = rtg_sqrtf(radicand);
+    const float u0 = (-b + root) / den;
+    const float u1 = (-b - root) / den;
+    if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+    if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
+  }
+  return sm;
+}
+
+// Closest hit, raytracer.h:145-194 (first index wins ties; minT starts 1000).
+template <class Scene>
+RTG_HD int closest_hit(const Scene& sc, V3 o, V3 d, float& tOut) {
+  const float a = vdot(d, d);
+  const float a4 = 4.0f * a;
+  const float den = 2.0f * a;
+  float minT = 1000.f;
+  int best = -1;
+  const unsigned n = sc.n;
+  for (unsigned i = 0; i < n; ++i) {
+    float r2;
+    V3 c = sc.sphere(i, r2);
+    bool res;
+    float t = ray_sphere(o, d, c, r2, a4, den, res);
+    if (res && t < minT) { minT = t; best = (int)i; }
+  }
+  tOut = minT;
+  return best;
+}
+
+// Shadow query, raytracer.h:272-309 (see header note for the early exit).
+template <class Scene>
+RTG_HD bool blocked(const Scene& sc, V3 o, V3 d, float gap) {
+  const float a = vdot(d, d);
+  const float a4 = 4.0f * a;
+  const float den = 2.0f * a;
+  const unsigned n = sc.n;
+  for (unsigned i = 0; i < n; ++i) {
+    float r2;
+    V3 c = sc.sphere(i, r2);
+    bool res;
+    float t = ray_sphere(o, d, c, r2, a4, den, res);
+    if (res && t < 1000.f) {
+      V3 dist = vsmul(t, d);
+      if (vdot(dist, dist) < gap) return true;
+    }
+  }
+  return false;
+}
+
+// raytracer.h:245-270
+template <class Scene>
+RTG_HD int primary_container(const Scene& sc, V3 pt) {
+  const unsigned n = sc.n;
+  for (unsigned i = 0; i < n; ++i) {
+    float r2;
+    V3 c = sc.sphere(i, r2);
+    V3 dist = vsub(pt, c);
+    if (vdot(dist, dist) <= sc.contain_r2(i)) return (int)i;
+  }
+  return -1;
+}
+
+// raytracer.h:313-367, with the incidence test hoisted ahead of the shadow ray.
+template <class Scene>
+RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
+  V3 sum = v3(0.f, 0.f, 0.f);
+  const unsigned m = sc.m;
+  for (unsigned l = 0; l < m; ++l) {
+    V3 Lpos, Lcol;
+    sc.light(l, Lpos, Lcol);
+    V3 dist = vsub(Lpos, P);
+    const float gap = vdot(dist, dist);
+    const V3 dir = vsmul(1.f / rtg_sqrtf(gap), dist);  // vnorm(dist)
+    const float incidence = vdot(N, dir);
+    if (incidence > 0.f) {
+      if (!blocked(sc, P, dir, gap)) {
+        const float intensity = incidence / gap;
+        sum = vadd(sum, vsmul(intensity, Lcol));
+      }
+    }
+  }
+  return sum;
+}
+
+// raytracer.h:370-403 (f64 island).
+RTG_HD float polarised_reflection(float n1, float n2, float cosA1, float cosA2) {
+  const float left = n1 * cosA1;
+  const float right = n2 * cosA2;
+  const double num = (double)(left - right);
+  double den = (double)(left + right);
+  den *= den;
+  if (den < (double)1.0e-6f) return 1.f;
+  float refl = (float)((num * num) / den);
+  if (refl > 1.f) refl = 1.f;
+  return refl;
+}
+
+// raytracer.h:642-815.  Computes the reflection factor R and, when wantRay,
+// the refracted direction.  Returns the target material index.
+template <class Scene>
+RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRay,
+                      V3& dirOut, float& R) {
+  float cosA1 = vdot(D, N);
+  float sinA1 = 0.f;
+  if (cosA1 <= -1.0f) { cosA1 = -1.f; sinA1 = 0.f; }
+  else if (cosA1 >= 1.f) { cosA1 = 1.f; sinA1 = 0.f; }
+  else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }
+
+  const V3 testPt = vadd(vsmul(0.01f, D), P);
+  int tgt = primary_container(sc, testPt);
+  if (tgt < 0) tgt = (int)sc.n;  // background material
+  const float nTgt = sc.refr(tgt);
+  const float ratio = nSrc / nTgt;
+  const float sinA2 = ratio * sinA1;
+
+  if (wantRay) {
+    // solveQuadratic(1, 2cosA1, 1 - 1/ratio^2), algebra.h:22-65 with a = 1.
+    const float qb = 2.f * cosA1;
+    const float qc = 1.f - (1.f / (ratio * ratio));
+    const float rad = (qb * qb) - ((4.f * 1.f) * qc);
+    float r0, r1;
+    int ns;
+    if (fabsf(rad) < 0.001f) {
+      r0 = -qb / (2.f * 1.f);
+      r1 = 0.f;
+      ns = 1;
+    } else {
+      const float root = rtg_sqrtf(rad);
+      const float den = 2.0f * 1.f;
+      r0 = (-qb + root) / den;
+      r1 = (-qb - root) / den;
+      ns = 2;
+    }
+    float maxAlign = (float)-0.1;
+    V3 dir = v3(0.f, 0.f, 0.f);
+    {
+      V3 cur = vadd(D, vsmul(r0, N));
+      float al = vdot(D, cur);
+      if (al > maxAlign) { maxAlign = al; dir = cur; }
+    }
+    if (ns == 2) {
+      V3 cur = vadd(D, vsmul(r1, N));
+      float al = vdot(D, cur);
+      if (al > maxAlign) { maxAlign = al; dir = cur; }
+    }
+    dirOut = dir;
+  }
+  float cosA2 = rtg_sqrtf(1.f - (sinA2 * sinA2));
+  if (cosA1 < 0.f) cosA2 = -cosA2;
+  const float Rs = polarised_reflection(nSrc, nTgt, cosA1, cosA2);
+  const float Rp = polarised_reflection(nSrc, nTgt, cosA2, cosA1);
+  R = (float)((double)(Rs + Rp) * 0.5);
+  return tgt;
+}
+
+// One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
+// raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
+template <int S, class Scene>
+RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
+  constexpr int NF = (S > 1) ? (S - 1) : 1;
+  Frame st[NF];
+  int sp = 0;                           // == level of the node being processed
+  V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
+  V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
+  int rm = (int)sc.n;                   // background material
+  for (;;) {
+    // ---------------- stage 0 (raytracer.h:454-550) ----------------
+    float t;
+    const int hit = closest_hit(sc, o, d, t);
+    if (hit < 0) {
+      ret = vmul(I, sc.mat(rm).matte);                       // :544
+    } else if (significant(I)) {                             // :460
+      float r2unused;
+      const V3 c = sc.sphere((unsigned)hit, r2unused);
+      const V3 P = vadd(o, vsmul(t, d));
+      const V3 N = vnorm(vsub(P, c));
+      const Mat mh = sc.mat(hit);
+      const float op = mh.opacity;
+      const float tr = 1.f - op;
+      V3 colour = v3(0.f, 0.f, 0.f);
+      if (op > 0.f) {
+        V3 tmp = vmul(I, mh.matte);
+        tmp = vsmul(op, tmp);
+        const V3 mc = matte_light(sc, P, N);
+        tmp = vmul(mc, tmp);
+        colour = vadd(tmp, colour);
+      }
+      if (tr > 0.f) {
+        const bool leaf = (sp >= S - 1);
+        const Mat mr = sc.mat(rm);
+        V3 cdir;
+        float R;
+        const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
+        // stage-1 reflection colour, raytracer.h:563-578
+        const float prod = tr * R;
+        V3 rc = vsmul(prod, v3(1.f, 1.f, 1.f));
+        rc = vadd(rc, vsmul(mr.opacity, mh.gloss));
+        rc = vmul(I, rc);
+        const bool sigR = significant(rc);
+        if (!leaf) {
+          Frame& f = st[sp < NF ? sp : NF - 1];
+          f.colour = colour;
+          f.rm = rm;
+          f.flags = sigR ? 2 : 0;
+          if (sigR) {
+            // calculateReflection, raytracer.h:817-842
+            const float perp = 2.f * vdot(d, N);
+            const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
+            f.rd = rd;
+            f.ro = vadd(P, vsmul(0.01f, rd));
+            f.rI = rc;
+          }
+          ++sp;
+          ret = colour;                                       // :538
+          // refraction child: calculateRefraction's refracted ray (:805-809)
+          I = vsmul((1.f - R), vsmul(tr, I));
+          o = P;
+          d = cdir;
+          rm = tgt;
+          continue;
+        }
+        // Leaf: both children dropped by the full stack.
+        const V3 c1 = vadd(colour, colour);
+        ret = sigR ? vadd(c1, c1) : c1;
+      } else {
+        ret = colour;
+      }
+    }
+    // else: hit but insignificant intensity -> ret unchanged (stale)
+
+    // ---------------- unwind (stages 1 and 2) ----------------
+    bool descend = false;
+    while (sp > 0) {
+      Frame& f = st[sp - 1 < NF ? sp - 1 : NF - 1];
+      f.colour = vadd(ret, f.colour);                         // :553 / :622
+      ret = f.colour;                                         // :617 / :626
+      if ((f.flags & 3) == 2) {                               // stage 1, reflection
+        f.flags = 1;                                          // -> stage 2
+        o = f.ro; d = f.rd; I = f.rI; rm = f.rm;
+        descend = true;
+        break;
+      }
+      --sp;
+    }
+    if (!descend) return ret;
+  }
+}
+
+// main.cpp:411-452 for pixel (x, y) of the frame.
+template <int S, class Scene>
+RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
+  const float pxX = (((float)x - cam.halfW)) * cam.xs;
+  const float pxY = (cam.halfH - (float)y) * cam.ys;
+  V3 pix = v3(0.f, 0.f, 0.f);
+  for (int i = 0; i < cam.nAA; ++i) {
+    for (int j = 0; j < cam.nAA; ++j) {
+      const float rx = (pxX + (float)(((float)j) * cam.st)) * cam.asp;
+      const float ry = (pxY + (float)(((float)i) * cam.st));
+      const V3 dir = vnorm(v3(rx, ry, cam.zoom));
+      V3 c = trace_sample<S>(sc, dir);
+      c = vsmul(cam.inv, c);
+      pix = vadd(pix, c);
+    }
+  }
+  return pix;
+}
+
+}  // namespace rtg

@@ -1,0 +1,280 @@
+"""rtg_amd — ctypes binding of librtg.so, the MI355X raytracer-gamma hot path.
+
+This is the binding a Python maintainer would add over the C ABI in
+include/rtg.h (INTEGRATION.md shows the C/C++ and ctypes forms).  It mirrors
+the reference's host interface for the path:
+
+  reference                                   here
+  ------------------------------------------  ------------------------------------
+  struct Sphere / Light / Material (C)        SPHERE_DTYPE / LIGHT_DTYPE / MATERIAL_DTYPE
+  setMatOpacity+setMatteGlossBalance+...      make_material()   (raytracer.h:53-74)
+  scene of main.cpp:104-168                   generate_scene()  (+ SURVEY §8d generator)
+  OpenCL raytrace kernel + enqueue/readback   render() / Context.render_device()
+    (raytrace_kernel.cl:870, main.cpp:277-468)
+  maxColourValuePixelBuffer (algebra.h:68)    max_colour_value()
+  savePPM (main.cpp:43-91)                    save_ppm() / ppm_bytes()
+
+There is no CPU fallback: every render call goes to the HIP kernel and raises
+RtgError when the library or a GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+# torch (when present) must own the HIP runtime of this process: librtg.so's
+# libamdhip64.so.7 dependency then resolves to the runtime torch already
+# loaded, so torch streams / pointers and ours are the same runtime's.
+try:  # pragma: no cover - import side effect only
+    import torch  # noqa: F401
+except Exception:  # torch absent: librtg loads /opt/rocm's runtime itself
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "librtg.so")
+
+VEC_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4")])
+MATERIAL_DTYPE = np.dtype([("matteColour", "<f4", 3), ("glossColour", "<f4", 3),
+                           ("opacity", "<f4"), ("refractiveIndex", "<f4")])
+SPHERE_DTYPE = np.dtype([("pos", "<f4", 3), ("radius", "<f4"), ("material", MATERIAL_DTYPE)])
+LIGHT_DTYPE = np.dtype([("pos", "<f4", 3), ("col", "<f4", 3)])
+assert VEC_DTYPE.itemsize == 12 and MATERIAL_DTYPE.itemsize == 32
+assert SPHERE_DTYPE.itemsize == 48 and LIGHT_DTYPE.itemsize == 24
+
+RTG_OK = 0
+ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory",
+          -4: "no such device", -5: "I/O error"}
+
+# Every symbol include/rtg.h declares (checked by tests/test_host.py).
+EXPORTED = [
+    "rtg_last_error", "rtg_abi_version", "rtg_device_count", "rtg_device_info",
+    "rtg_render", "rtg_context_create", "rtg_context_destroy", "rtg_context_set_scene",
+    "rtg_shard_rows", "rtg_shard_global_row", "rtg_render_device", "rtg_render_rows_device",
+    "rtg_render_rows", "rtg_set_launch_opts",
+    "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
+    "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate",
+]
+
+
+class RtgError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load librtg.so (built in-tree by `make -C raytracer-gamma_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtgError(f"librtg.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u, i, f, sz = ctypes.c_void_p, ctypes.c_uint, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+        L.rtg_last_error.restype = ctypes.c_char_p
+        L.rtg_abi_version.restype = i
+        L.rtg_device_count.argtypes = [ctypes.POINTER(i)]
+        L.rtg_device_info.argtypes = [i, ctypes.c_char_p, sz]
+        L.rtg_render.argtypes = [i, vp, u, vp, u, u, u, f, f, i, vp]
+        L.rtg_context_create.argtypes = [i, ctypes.POINTER(vp)]
+        L.rtg_context_destroy.argtypes = [vp]
+        L.rtg_context_set_scene.argtypes = [vp, vp, u, vp, u]
+        L.rtg_shard_rows.argtypes = [u, u, u, u, ctypes.POINTER(u)]
+        L.rtg_shard_global_row.argtypes = [u, u, u, u]
+        L.rtg_shard_global_row.restype = u
+        L.rtg_render_device.argtypes = [vp, u, u, f, f, i, u, u, u, vp, vp]
+        L.rtg_render_rows_device.argtypes = [vp, u, u, f, f, i, vp, u, vp, vp]
+        L.rtg_render_rows.argtypes = [i, vp, u, vp, u, u, u, f, f, i, vp, u, vp]
+        L.rtg_set_launch_opts.argtypes = [vp, vp]
+        L.rtg_max_colour.argtypes = [vp, sz]
+        L.rtg_max_colour.restype = f
+        L.rtg_max_colour_device.argtypes = [vp, vp, sz, vp, vp]
+        L.rtg_ppm_bytes.argtypes = [vp, sz, f, vp]
+        L.rtg_ppm_bytes.restype = None
+        L.rtg_ppm_bytes_device.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.rtg_save_ppm.argtypes = [vp, ctypes.c_char_p, i, i, f]
+        L.rtg_make_material.argtypes = [f, f, vp, vp, f, vp]
+        L.rtg_make_material.restype = None
+        L.rtg_scene_generate.argtypes = [ctypes.c_ulonglong, u, u, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != RTG_OK:
+        msg = lib().rtg_last_error().decode(errors="replace")
+        raise RtgError(f"{what}: {ERRORS.get(rc, rc)}: {msg}")
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+# ---------------------------------------------------------------- scene helpers
+def make_material(opacity, gloss_factor, matte, gloss, refractive_index):
+    """setMatOpacity + setMatteGlossBalance + setMatRefractivityIndex (raytracer.h:53-74)."""
+    out = np.zeros(1, MATERIAL_DTYPE)
+    m = np.asarray(matte, np.float32)
+    g = np.asarray(gloss, np.float32)
+    lib().rtg_make_material(float(opacity), float(gloss_factor), _ptr(m), _ptr(g),
+                            float(refractive_index), _ptr(out))
+    return out[0]
+
+
+def generate_scene(n_spheres: int, n_lights: int, seed: int = 42):
+    """main.cpp:104-168 scene, extended by the seeded generator of SURVEY.md §8d."""
+    sph = np.zeros(n_spheres, SPHERE_DTYPE)
+    lgt = np.zeros(n_lights, LIGHT_DTYPE)
+    _check(lib().rtg_scene_generate(seed, n_spheres, n_lights, _ptr(sph), _ptr(lgt)),
+           "rtg_scene_generate")
+    return sph, lgt
+
+
+def reference_scene():
+    """The scene hard-coded in main.cpp:104-168 (3 spheres, 2 lights)."""
+    return generate_scene(3, 2)
+
+
+# ---------------------------------------------------------------- output helpers
+def max_colour_value(fb: np.ndarray) -> float:
+    """maxColourValuePixelBuffer, algebra.h:68-91."""
+    fb = np.ascontiguousarray(fb, np.float32)
+    return float(lib().rtg_max_colour(_ptr(fb), fb.size // 3))
+
+
+def ppm_bytes(fb: np.ndarray, max_colour: float) -> np.ndarray:
+    fb = np.ascontiguousarray(fb, np.float32)
+    out = np.empty(fb.size, np.uint8)
+    lib().rtg_ppm_bytes(_ptr(fb), fb.size // 3, float(max_colour), _ptr(out))
+    return out
+
+
+def ppm_file_bytes(fb: np.ndarray, max_colour: float | None = None) -> bytes:
+    """Exact bytes savePPM (main.cpp:43-91) writes for an (H, W, 3) framebuffer."""
+    h, w = fb.shape[0], fb.shape[1]
+    mx = max_colour_value(fb) if max_colour is None else max_colour
+    return b"P6\n%d %d\n255\n" % (w, h) + ppm_bytes(fb, mx).tobytes()
+
+
+def save_ppm(fb: np.ndarray, filename: str, max_colour: float | None = None) -> None:
+    fb = np.ascontiguousarray(fb, np.float32)
+    mx = max_colour_value(fb) if max_colour is None else max_colour
+    _check(lib().rtg_save_ppm(_ptr(fb), filename.encode(), fb.shape[1], fb.shape[0], mx),
+           "rtg_save_ppm")
+
+
+def shard_rows(height: int, row_block: int, shard: int, n_shards: int) -> int:
+    r = ctypes.c_uint(0)
+    _check(lib().rtg_shard_rows(height, row_block, shard, n_shards, ctypes.byref(r)),
+           "rtg_shard_rows")
+    return r.value
+
+
+def shard_row_indices(height: int, row_block: int, shard: int, n_shards: int) -> np.ndarray:
+    n = shard_rows(height, row_block, shard, n_shards)
+    f = lib().rtg_shard_global_row
+    return np.array([f(k, row_block, shard, n_shards) for k in range(n)], np.int64)
+
+
+# ---------------------------------------------------------------- device
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    _check(lib().rtg_device_count(ctypes.byref(c)), "rtg_device_count")
+    return c.value
+
+
+def device_info(device: int = 0) -> str:
+    buf = ctypes.create_string_buffer(256)
+    _check(lib().rtg_device_info(device, buf, 256), "rtg_device_info")
+    return buf.value.decode()
+
+
+def render(spheres, lights, width: int, height: int, zoom: float = -4.0,
+           alias_factor: float = 3.0, stack_size: int = 6, device: int = 0) -> np.ndarray:
+    """One-shot drop-in for the reference's GPU launch (main.cpp:277-468):
+    returns the (H, W, 3) float32 framebuffer of the reference CPU path."""
+    spheres = np.ascontiguousarray(spheres, SPHERE_DTYPE)
+    lights = np.ascontiguousarray(lights, LIGHT_DTYPE)
+    out = np.empty((height, width, 3), np.float32)
+    _check(lib().rtg_render(device, _ptr(spheres), len(spheres), _ptr(lights), len(lights),
+                            width, height, float(zoom), float(alias_factor), stack_size,
+                            _ptr(out)), "rtg_render")
+    return out
+
+
+def render_rows(spheres, lights, width: int, height: int, rows, zoom: float = -4.0,
+                alias_factor: float = 3.0, stack_size: int = 6, device: int = 0) -> np.ndarray:
+    """Render only the listed global rows; returns (len(rows), W, 3)."""
+    spheres = np.ascontiguousarray(spheres, SPHERE_DTYPE)
+    lights = np.ascontiguousarray(lights, LIGHT_DTYPE)
+    rows = np.ascontiguousarray(rows, np.uint32)
+    out = np.empty((len(rows), width, 3), np.float32)
+    _check(lib().rtg_render_rows(device, _ptr(spheres), len(spheres), _ptr(lights),
+                                 len(lights), width, height, float(zoom), float(alias_factor),
+                                 stack_size, _ptr(rows), len(rows), _ptr(out)),
+           "rtg_render_rows")
+    return out
+
+
+class Context:
+    """Persistent device context: scene resident in HBM, renders into caller
+    device memory (e.g. a torch tensor's data_ptr()) on a caller stream."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().rtg_context_create(device, ctypes.byref(self._h)), "rtg_context_create")
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().rtg_context_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, spheres, lights):
+        self._sph = np.ascontiguousarray(spheres, SPHERE_DTYPE)
+        self._lgt = np.ascontiguousarray(lights, LIGHT_DTYPE)
+        _check(lib().rtg_context_set_scene(self._h, _ptr(self._sph), len(self._sph),
+                                           _ptr(self._lgt), len(self._lgt)),
+               "rtg_context_set_scene")
+
+    def set_variant(self, variant: int):
+        opts = (ctypes.c_int * 8)(variant, 0, 0, 0, 0, 0, 0, 0)
+        _check(lib().rtg_set_launch_opts(self._h, ctypes.cast(opts, ctypes.c_void_p)),
+               "rtg_set_launch_opts")
+
+    def render_device(self, width, height, dst_ptr: int, zoom=-4.0, alias_factor=3.0,
+                      stack_size=6, row_block=16, shard=0, n_shards=1, stream: int = 0):
+        _check(lib().rtg_render_device(self._h, width, height, float(zoom),
+                                       float(alias_factor), stack_size, row_block, shard,
+                                       n_shards, ctypes.c_void_p(dst_ptr),
+                                       ctypes.c_void_p(stream) if stream else None),
+               "rtg_render_device")
+
+    def max_colour_device(self, src_ptr: int, n_pixels: int, dst_ptr: int, stream: int = 0):
+        _check(lib().rtg_max_colour_device(self._h, ctypes.c_void_p(src_ptr), n_pixels,
+                                           ctypes.c_void_p(dst_ptr),
+                                           ctypes.c_void_p(stream) if stream else None),
+               "rtg_max_colour_device")
+
+    def ppm_bytes_device(self, src_ptr: int, n_pixels: int, max_ptr: int, dst_ptr: int,
+                         stream: int = 0):
+        _check(lib().rtg_ppm_bytes_device(self._h, ctypes.c_void_p(src_ptr), n_pixels,
+                                          ctypes.c_void_p(max_ptr), ctypes.c_void_p(dst_ptr),
+                                          ctypes.c_void_p(stream) if stream else None),
+               "rtg_ppm_bytes_device")
+
+
+def canonical_bits(fb: np.ndarray) -> np.ndarray:
+    """uint32 view with every NaN mapped to the x86 default NaN 0xFFC00000."""
+    b = np.ascontiguousarray(fb, np.float32).view(np.uint32).copy()
+    b[np.isnan(np.ascontiguousarray(fb, np.float32))] = 0xFFC00000
+    return b

@@ -1,0 +1,157 @@
+"""CPU tests of librtg.so's host side: ABI surface, scene construction, PPM
+writer, colour max, row sharding and error behaviour.  No GPU calls."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, P, PKG, ROOT, load_scene, md5
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "rtg.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rtg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol(rtg):
+    declared = _declared_functions()
+    assert len(declared) >= 20
+    lib = rtg.lib()
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(rtg.EXPORTED) == declared
+    assert lib.rtg_abi_version() == 1
+
+
+def test_struct_layouts_match_reference(rtg):
+    # vec.h / material.h / sphere.h / raytracer.h:20-25 (also static_asserted in C++)
+    assert rtg.SPHERE_DTYPE.fields["radius"][1] == 12
+    assert rtg.SPHERE_DTYPE.fields["material"][1] == 16
+    assert rtg.MATERIAL_DTYPE.fields["opacity"][1] == 24
+    assert rtg.MATERIAL_DTYPE.fields["refractiveIndex"][1] == 28
+    assert rtg.LIGHT_DTYPE.fields["col"][1] == 12
+
+
+@pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
+def test_scene_generator_matches_golden(rtg, golden, name):
+    c = golden["configs"][name]
+    sph, lg = rtg.generate_scene(c["spheres"], c["lights"], 42)
+    gs, gl = load_scene(name, c["spheres"], c["lights"])
+    assert sph.tobytes() == gs.tobytes()
+    assert lg.tobytes() == gl.tobytes()
+    assert md5(sph.tobytes() + lg.tobytes()) == c["scene_md5"]
+
+
+def test_main_cpp_materials(rtg):
+    """main.cpp:126-145 via setMatteGlossBalance's double-precision factor."""
+    sph, _ = rtg.reference_scene()
+    m0 = sph[0]["material"]
+    k = np.float32(1.0 - np.float64(np.float32(0.2)))
+    assert m0["matteColour"][0] == k * np.float32(0.4)
+    assert m0["glossColour"][1] == np.float32(0.2) * np.float32(1.0)
+    assert m0["opacity"] == np.float32(0.8) and m0["refractiveIndex"] == np.float32(1.55)
+    assert list(sph["radius"]) == [5.0, 2.0, 3.0]
+
+
+def test_scene_generator_seeds_differ(rtg):
+    a, _ = rtg.generate_scene(16, 3, 42)
+    b, _ = rtg.generate_scene(16, 3, 43)
+    assert a[:3].tobytes() == b[:3].tobytes()  # fixed main.cpp spheres
+    assert a[3:].tobytes() != b[3:].tobytes()
+
+
+def _special_floats(rng, n):
+    v = rng.standard_normal(n).astype(np.float32) * np.float32(1e-4)
+    specials = np.array([0.0, -0.0, np.nan, -np.nan, np.inf, -np.inf, 1.0, 2.0, 1e-38, 1e30,
+                         -1e30, 0.99999994, 1.0000001, 7e-5, -7e-5, 3e38], np.float32)
+    v[: len(specials)] = specials
+    v[len(specials):len(specials) + 64] = rng.uniform(-2, 2, 64).astype(np.float32)
+    return v
+
+
+def test_ppm_bytes_match_oracle(rtg, oracle):
+    rng = np.random.default_rng(3)
+    fb = _special_floats(rng, 3 * 5000).reshape(-1, 3)
+    for mx in [6.955025e-05, 1.0, 3.0535437e-05, 1e-30, 2.5]:
+        a = rtg.ppm_bytes(fb, mx)
+        b = oracle.ppm_bytes(fb, mx)
+        assert (a == b).all()
+
+
+def test_max_colour_matches_oracle(rtg, oracle):
+    rng = np.random.default_rng(4)
+    fb = _special_floats(rng, 3 * 777).reshape(-1, 3)
+    fb[np.isinf(fb)] = 0  # keep a finite max for the second check below
+    assert rtg.max_colour_value(fb) == oracle.max_colour(fb)
+    assert rtg.max_colour_value(np.zeros((10, 3), np.float32)) == 1.0   # algebra.h:86-88
+    assert rtg.max_colour_value(np.full((4, 3), np.nan, np.float32)) == 1.0
+    assert rtg.max_colour_value(-np.ones((4, 3), np.float32)) == 1.0
+
+
+@pytest.mark.parametrize("name", ["ref800", "c1"])
+def test_save_ppm_matches_golden(rtg, oracle, golden, tmp_path, name):
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
+    fb = oracle.render(sph, lg, c["W"], c["H"], c["stack_size"])
+    path = str(tmp_path / "out.ppm")
+    rtg.save_ppm(fb, path)
+    data = open(path, "rb").read()
+    assert data[:15] == b"P6\n%d %d\n255\n" % (c["W"], c["H"])[:15]
+    assert md5(data) == c["ppm_md5"]
+    assert md5(rtg.ppm_file_bytes(fb)) == c["ppm_md5"]
+
+
+def test_save_ppm_errors(rtg, tmp_path):
+    with pytest.raises(rtg.RtgError):
+        rtg.save_ppm(np.zeros((0, 4, 3), np.float32), str(tmp_path / "x.ppm"))
+    with pytest.raises(rtg.RtgError):
+        rtg.save_ppm(np.zeros((2, 2, 3), np.float32), str(tmp_path / "nodir" / "x.ppm"))
+
+
+@pytest.mark.parametrize("H,B,G", [(2160, 16, 1), (2160, 16, 2), (2160, 16, 8), (2160, 8, 7),
+                                   (600, 16, 3), (1, 16, 8), (17, 4, 5), (4320, 16, 8),
+                                   (100, 1, 3), (33, 32, 2)])
+def test_shard_rows_partition_frame(rtg, H, B, G):
+    seen = []
+    for g in range(G):
+        rows = rtg.shard_row_indices(H, B, g, G)
+        assert (np.diff(rows) > 0).all() if len(rows) > 1 else True
+        for r in rows:
+            assert (r // B) % G == g
+        seen.extend(rows.tolist())
+    assert sorted(seen) == list(range(H))
+
+
+def test_shard_rows_invalid(rtg):
+    with pytest.raises(rtg.RtgError):
+        rtg.shard_rows(100, 0, 0, 1)
+    with pytest.raises(rtg.RtgError):
+        rtg.shard_rows(100, 16, 2, 2)
+
+
+def test_render_entry_points_reject_bad_arguments_without_gpu(rtg):
+    L = rtg.lib()
+    # null context / scene: validated before any HIP call
+    assert L.rtg_render_device(None, 8, 8, ctypes.c_float(-4), ctypes.c_float(3), 6, 16, 0, 1,
+                               None, None) == -1
+    assert L.rtg_render_rows_device(None, 8, 8, ctypes.c_float(-4), ctypes.c_float(3), 6,
+                                    None, 3, None, None) == -1
+    assert L.rtg_render(0, None, 0, None, 0, 4, 4, ctypes.c_float(-4), ctypes.c_float(3), 6,
+                        None) == -1
+    assert b"null" in L.rtg_last_error()
+    assert L.rtg_context_set_scene(None, None, 0, None, 0) == -1
+
+
+def test_host_driver_builds_and_prints_help():
+    exe = os.path.join(PKG, "rtg_main")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", PKG, "rtg_main"], check=True)
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    assert "--width" in r.stdout and "--device" in r.stdout

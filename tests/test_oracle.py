@@ -1,0 +1,183 @@
+"""CPU tests: the oracle (C restatement of raytracer.h) is pinned against the
+reference's own output, and the kernel's restructured traversal (compiled for
+the host, tests/hostsim) is checked bit for bit against the oracle.
+
+Pinning sources, strongest first:
+  * oracle/_ref/librtgref_S*.so — the reference compiled from /root/reference
+    (present only in the build container; those tests skip elsewhere);
+  * tests/golden/ — fixtures the reference produced (tests/golden/make_golden.py),
+    including SURVEY.md §8c's known answers for the main.cpp scene.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import (BUILD, GOLDEN, P, ROOT, bits_equal, canon_md5, first_mismatch,
+                      load_f32, load_scene, md5, random_scene)
+
+REF_DIR = os.path.join(ROOT, "oracle", "_ref")
+HAVE_REF = os.path.exists(os.path.join(REF_DIR, "librtgref_S6.so")) and \
+    os.path.exists("/root/reference/raytracer_gamma/raytracer.h")
+
+# SURVEY.md §8c known answers (recorded during the survey, before this build).
+SURVEY_KNOWN = {
+    "ref800": ("96b20332f1c1fdf97efec7da14a0d920", "77a498a83918ef392d1f080532d1f4dc"),
+    "c1": ("de44ee1fbd894f8c734db17a8878ad08", "53f45653f638bf19d6d66c5775e85807"),
+}
+
+
+def test_survey_known_answers_in_golden(golden):
+    for name, (fb, ppm) in SURVEY_KNOWN.items():
+        assert golden["configs"][name]["fb_md5_raw"] == fb
+        assert golden["configs"][name]["fb_md5"] == fb  # all NaNs already 0xFFC00000
+        assert golden["configs"][name]["ppm_md5"] == ppm
+    assert golden["configs"]["ref800"]["nan_values"] > 0  # TIR NaNs are exercised
+
+
+@pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
+def test_oracle_small_frames(oracle, golden, name):
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
+    sw, sh = c["small"]["W"], c["small"]["H"]
+    want = load_f32(os.path.join(GOLDEN, f"{name}.small.f32"), (sh, sw, 3))
+    got = oracle.render(sph, lg, sw, sh, c["stack_size"])
+    assert bits_equal(got, want), first_mismatch(got, want)
+
+
+@pytest.mark.parametrize("name", ["ref800", "c1"])
+def test_oracle_full_frame_md5(oracle, golden, rtg, name):
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
+    fb = oracle.render(sph, lg, c["W"], c["H"], c["stack_size"])
+    assert canon_md5(fb) == c["fb_md5"]
+    assert oracle.counters[0] == c["ray_sphere_tests"]
+    mx = oracle.max_colour(fb)
+    assert np.float32(mx).view(np.uint32) == c["max_colour_bits"]
+    ppm = b"P6\n%d %d\n255\n" % (c["W"], c["H"]) + oracle.ppm_bytes(fb, mx).tobytes()
+    assert md5(ppm) == c["ppm_md5"]
+
+
+def test_oracle_sampled_rows(oracle, golden):
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    rows = c["rows"]["rows"]
+    want = load_f32(os.path.join(GOLDEN, "c2.rows.f32"), (len(rows), c["W"], 3))
+    got = oracle.render(sph, lg, c["W"], c["H"], c["stack_size"], rows=rows)
+    assert bits_equal(got, want), first_mismatch(got, want)
+
+
+def _cases(golden):
+    return [(k, c) for k, c in enumerate(golden["cases"])]
+
+
+def test_oracle_edge_cases(oracle, golden):
+    for c in golden["cases"]:
+        sph, lg = load_scene(c["name"], c["spheres"], c["lights"])
+        want = load_f32(os.path.join(GOLDEN, c["name"] + ".f32"), (c["H"], c["W"], 3))
+        got = oracle.render(sph, lg, c["W"], c["H"], c["stack_size"], aa=c["aliasFactor"],
+                            zoom=c["zoom"])
+        assert bits_equal(got, want), (c["name"], first_mismatch(got, want))
+        assert oracle.counters[0] == c["ray_sphere_tests"]
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="reference build (oracle/_ref) not present")
+def test_oracle_vs_reference_random_scenes(oracle, rtg):
+    rng = np.random.default_rng(7)
+    for trial in range(30):
+        S = int(rng.integers(1, 10))
+        n, m = int(rng.integers(0, 14)), int(rng.integers(0, 5))
+        W, H = int(rng.integers(1, 48)), int(rng.integers(1, 36))
+        aa = float(rng.choice([1.0, 2.0, 3.0, 2.5, 4.0]))
+        zoom = float(rng.choice([-4.0, -2.0, -7.0]))
+        sph, lg = random_scene(rng, n, m)
+        ref = ctypes.CDLL(os.path.join(REF_DIR, f"librtgref_S{S}.so"))
+        assert ref.ref_stack_size() == S
+        rows = np.arange(H, dtype=np.uint32)
+        want = np.zeros((H, W, 3), np.float32)
+        ref.ref_render_rows(P(sph), n, P(lg), m, W, H, ctypes.c_float(zoom), ctypes.c_float(aa),
+                            P(rows), H, P(want), 4)
+        got = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
+        assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="reference build (oracle/_ref) not present")
+def test_reference_struct_layout(rtg):
+    ref = ctypes.CDLL(os.path.join(REF_DIR, "librtgref_S6.so"))
+    sizes = [ref.ref_sizeof(i) for i in range(6)]
+    assert sizes == [12, 36, 32, 48, 24, 76]
+    assert rtg.SPHERE_DTYPE.itemsize == sizes[3] and rtg.LIGHT_DTYPE.itemsize == sizes[4]
+    assert rtg.MATERIAL_DTYPE.itemsize == sizes[2]
+
+
+# ------------------------------------------------------------------ hostsim
+@pytest.fixture(scope="session")
+def hostsim():
+    """Host build of the kernel's traversal (rtg_trace.h), test-only."""
+    os.makedirs(BUILD, exist_ok=True)
+    so = os.path.join(BUILD, "libhostsim.so")
+    src = os.path.join(ROOT, "tests", "hostsim", "hostsim.cpp")
+    deps = [src] + [os.path.join(ROOT, "raytracer-gamma_amd", "csrc", f) for f in
+                    ("rtg_trace.h", "rtg_scene_pack.h", "rtg_internal.h")]
+    if not os.path.exists(so) or any(os.path.getmtime(d) > os.path.getmtime(so) for d in deps):
+        subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fno-fast-math", "-std=c++17",
+                        "-fPIC", "-shared", "-I" + os.path.join(ROOT, "include"),
+                        "-I" + os.path.join(ROOT, "raytracer-gamma_amd", "csrc"), src, "-o", so],
+                       check=True)
+    return ctypes.CDLL(so)
+
+
+def _hostsim_render(hs, sph, lg, W, H, S, aa=3.0, zoom=-4.0, rows=None):
+    rows = np.arange(H, dtype=np.uint32) if rows is None else np.asarray(rows, np.uint32)
+    out = np.zeros((len(rows), W, 3), np.float32)
+    rc = hs.hostsim_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(zoom),
+                                ctypes.c_float(aa), S, P(rows), len(rows), P(out))
+    assert rc == 0
+    return out
+
+
+@pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
+def test_kernel_traversal_small_frames(hostsim, golden, name):
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
+    sw, sh = c["small"]["W"], c["small"]["H"]
+    want = load_f32(os.path.join(GOLDEN, f"{name}.small.f32"), (sh, sw, 3))
+    got = _hostsim_render(hostsim, sph, lg, sw, sh, c["stack_size"])
+    assert bits_equal(got, want), first_mismatch(got, want)
+
+
+def test_kernel_traversal_edge_cases(hostsim, golden):
+    for c in golden["cases"]:
+        if c["stack_size"] > 12:
+            continue  # hostsim instantiates S <= 12
+        sph, lg = load_scene(c["name"], c["spheres"], c["lights"])
+        want = load_f32(os.path.join(GOLDEN, c["name"] + ".f32"), (c["H"], c["W"], 3))
+        got = _hostsim_render(hostsim, sph, lg, c["W"], c["H"], c["stack_size"],
+                              aa=c["aliasFactor"], zoom=c["zoom"])
+        assert bits_equal(got, want), (c["name"], first_mismatch(got, want))
+
+
+def test_kernel_traversal_random_scenes(hostsim, oracle, rtg):
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        S = int(rng.integers(1, 13))
+        n, m = int(rng.integers(0, 14)), int(rng.integers(0, 5))
+        W, H = int(rng.integers(1, 40)), int(rng.integers(1, 30))
+        aa = float(rng.choice([1.0, 2.0, 3.0, 2.5]))
+        zoom = float(rng.choice([-4.0, -2.0, -7.0]))
+        sph, lg = random_scene(rng, n, m)
+        want = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
+        got = _hostsim_render(hostsim, sph, lg, W, H, S, aa=aa, zoom=zoom)
+        assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
+
+
+def test_kernel_traversal_c1_full_frame(hostsim, golden):
+    """A whole BASELINE config frame through the kernel's traversal (md5)."""
+    c = golden["configs"]["c1"]
+    sph, lg = load_scene("c1", c["spheres"], c["lights"])
+    got = _hostsim_render(hostsim, sph, lg, c["W"], c["H"], c["stack_size"])
+    assert canon_md5(got) == c["fb_md5"]
