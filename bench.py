@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--row-block", type=int, default=16)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--ab", default="", help="comma list of kernel variants to A/B after the "
+                    "timed run (interleaved rounds, kernel time via HIP events)")
+    ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -181,6 +184,28 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     mpx = W * H / (elapsed / args.steps) / 1e6
+
+    ab = None
+    if args.ab and world == 1:
+        variants = [int(v) for v in args.ab.split(",")]
+        times = {v: [] for v in variants}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(args.ab_rounds):
+            for v in variants:
+                ctx.set_variant(v)
+                ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B,
+                                  stream=sptr)  # warm
+                e0.record(stream)
+                for _ in range(3):
+                    ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B,
+                                      stream=sptr)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / 3)
+        ctx.set_variant(args.variant)
+        ab = {str(v): {"median_ms": round(float(np.median(t)), 4),
+                       "min_ms": round(float(np.min(t)), 4)} for v, t in times.items()}
+        log("A/B", ab)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -259,6 +284,7 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "gpu_vs_cpu": round(mpx / cpu["value"], 1) if cpu else None,
         "parity": parity,
+        "ab": ab,
     }
     print(json.dumps(out), flush=True)
     ctx.close()

@@ -16,6 +16,7 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -66,6 +67,15 @@ struct DevScene {
     r2 = g[3];
     return v3(g[0], g[1], g[2]);
   }
+  // Four consecutive sphere records: one 64-byte scalar load.
+  __device__ __forceinline__ void sphere4(unsigned i, V3* c, float* r2) const {
+    cfloat_p g = geom + 4 * i;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
+      r2[k] = g[4 * k + 3];
+    }
+  }
   __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
   __device__ __forceinline__ Mat mat(int i) const {
     const auto p = mats + 8 * i;
@@ -101,7 +111,7 @@ __device__ __forceinline__ float canon_nan(float v) {
   return (v != v) ? __uint_as_float(0xFFC00000u) : v;
 }
 
-template <int S, bool kLdsMats>
+template <int S, bool kLdsMats, int kVariant>
 __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   extern __shared__ float lmats[];  // (n+1)*8 floats when kLdsMats
   typedef typename std::conditional<kLdsMats, const float*, cfloat_p>::type MatPtr;
@@ -126,7 +136,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   if (x >= a.W || lr >= a.rowsLocal) return;
   const unsigned gy =
       a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
-  const V3 pix = shade_pixel<S>(sc, a.cam, x, gy);
+  const V3 pix = (kVariant == 1) ? shade_pixel<S>(sc, a.cam, x, gy)
+                                 : shade_pixel_persistent<S>(sc, a.cam, x, gy);
   float* o = a.dst + ((size_t)lr * a.W + x) * 3;
   o[0] = canon_nan(pix.x);
   o[1] = canon_nan(pix.y);
@@ -173,12 +184,17 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 }
 
 typedef void (*TraceFn)(const KernelArgs);
+// variant 0 (default) = persistent state machine (shade_pixel_persistent);
+// variant 1 = per-sample recursion (shade_pixel), kept for A/B measurement.
 template <int S>
-static TraceFn trace_fn(bool lds) { return lds ? trace_kernel<S, true> : trace_kernel<S, false>; }
+static TraceFn trace_fn(bool lds, int variant) {
+  if (variant == 1) return lds ? trace_kernel<S, true, 1> : trace_kernel<S, false, 1>;
+  return lds ? trace_kernel<S, true, 0> : trace_kernel<S, false, 0>;
+}
 
-static TraceFn pick_trace(int S, bool lds) {
+static TraceFn pick_trace(int S, bool lds, int variant) {
   switch (S) {
-#define RTG_CASE(k) case k: return trace_fn<k>(lds);
+#define RTG_CASE(k) case k: return trace_fn<k>(lds, variant);
     RTG_CASE(1) RTG_CASE(2) RTG_CASE(3) RTG_CASE(4) RTG_CASE(5) RTG_CASE(6) RTG_CASE(7)
     RTG_CASE(8) RTG_CASE(9) RTG_CASE(10) RTG_CASE(11) RTG_CASE(12) RTG_CASE(13)
     RTG_CASE(14) RTG_CASE(15) RTG_CASE(16)
@@ -249,6 +265,7 @@ int rtg_context_create(int device, rtg_context** out) {
   HIP_TRY(hipSetDevice(device));
   rtg_context* c = new rtg_context();
   c->device = device;
+  if (const char* v = getenv("RTG_VARIANT")) c->opts.variant = atoi(v);  // A/B knob
   if (hipMalloc(&c->maxScratch, 4) != hipSuccess) {
     delete c;
     rtg_set_error("hipMalloc failed");
@@ -321,7 +338,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     return RTG_ERR_INVALID;
   }
   const bool ldsMats = ctx->n + 1 <= kLdsMatMax;
-  TraceFn fn = pick_trace(stackSize, ldsMats);
+  TraceFn fn = pick_trace(stackSize, ldsMats, ctx->opts.variant);
   if (!fn) {
     rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
     return RTG_ERR_INVALID;

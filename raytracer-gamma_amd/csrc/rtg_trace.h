@@ -337,6 +337,258 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// v2: persistent per-lane state machine.
+//
+// Each iteration of the outer loop performs exactly ONE ray query for every
+// lane that still has work: the closest hit of a tree node's ray, or the
+// shadow ray of one light (raytracer.h:272-309, answered from the closest hit
+// of that ray: blocked iff a hit exists and |t*D|^2 < gap — literally the
+// reference's test).  The bookkeeping between queries (shading, refraction,
+// frame push/pop, moving on to the next light / node / sample) runs after the
+// query and leaves the lane with its next query.  So the sphere loop, where
+// the time goes, runs with every unfinished lane of the wave active whatever
+// stage of its Whitted tree or which of its 9 samples each lane is in, instead
+// of idling lanes whose tree was shallower (v1 above).
+//
+// Closest-hit query over all spheres, 4 per step (one 64-byte scalar load
+// when the scene supports it), first index wins ties: raytracer.h:145-194.
+template <class Scene>
+RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
+  const float a = vdot(d, d);
+  const float a4 = 4.0f * a;
+  const float den = 2.0f * a;
+  float minT = 1000.f;
+  int best = -1;
+  const unsigned n = sc.n;
+  unsigned i = 0;
+  for (; i + 4 <= n; i += 4) {
+    V3 c[4];
+    float r2[4];
+    sc.sphere4(i, c, r2);
+    float b[4], rad[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const V3 disp = vsub(o, c[k]);
+      b[k] = 2.0f * vdot(d, disp);
+      const float cc = vdot(disp, disp) - r2[k];
+      rad[k] = (b[k] * b[k]) - (a4 * cc);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (rad[k] >= 0.0f) {
+        const float root = rtg_sqrtf(rad[k]);
+        const float u0 = (-b[k] + root) / den;
+        const float u1 = (-b[k] - root) / den;
+        float sm = 10000.f;
+        bool res = false;
+        if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+        if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
+        if (res && sm < minT) { minT = sm; best = (int)(i + k); }
+      }
+    }
+  }
+  for (; i < n; ++i) {
+    float r2;
+    V3 c = sc.sphere(i, r2);
+    bool res;
+    float t = ray_sphere(o, d, c, r2, a4, den, res);
+    if (res && t < minT) { minT = t; best = (int)i; }
+  }
+  tOut = minT;
+  return best;
+}
+
+template <int S, class Scene>
+RTG_HD V3 shade_pixel_persistent(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
+  constexpr int NF = (S > 1) ? (S - 1) : 1;
+  enum : int { kClosest = 0, kShadow = 1, kDone = 2 };
+  const float pxX = (((float)x - cam.halfW)) * cam.xs;
+  const float pxY = (cam.halfH - (float)y) * cam.ys;
+  const int nSamples = cam.nAA * cam.nAA;
+  V3 pix = v3(0.f, 0.f, 0.f);
+  if (nSamples == 0) return pix;
+
+  Frame st[NF];
+  int sp = 0;                       // level of the current node
+  int s = 0;                        // sample index, i = s / nAA, j = s % nAA
+  V3 ret = v3(0.f, 0.f, 0.f);       // colourSum register
+  V3 d, I;                          // current node ray (origin lives in qo)
+  int rm = (int)sc.n;               // refractive material of the node
+  V3 qo = v3(0.f, 0.f, 0.f), qd;    // the lane's pending query ray
+  int phase = kClosest;
+  // hit-node shading state (valid while phase == kShadow / within an iteration)
+  V3 P = v3(0.f, 0.f, 0.f), N = v3(0.f, 0.f, 0.f), msum = v3(0.f, 0.f, 0.f);
+  int hit = 0, li = 0;
+  float lgap = 0.f, linc = 0.f;
+
+  // primary ray of sample 0 (main.cpp:432-436)
+  {
+    const float rx = (pxX + (float)(((float)0) * cam.st)) * cam.asp;
+    const float ry = (pxY + (float)(((float)0) * cam.st));
+    d = vnorm(v3(rx, ry, cam.zoom));
+    I = v3(1.f, 1.f, 1.f);
+    qd = d;
+  }
+
+  while (phase != kDone) {
+    float t;
+    const int best = closest_hit4(sc, qo, qd, t);
+
+    bool nextLight = false, afterMatte = false, unwind = false;
+    if (phase == kClosest) {
+      if (best < 0) {
+        ret = vmul(I, sc.mat(rm).matte);                    // raytracer.h:544
+        unwind = true;
+      } else if (!significant(I)) {
+        unwind = true;                                      // stale ret
+      } else {
+        float r2unused;
+        const V3 c = sc.sphere((unsigned)best, r2unused);
+        P = vadd(qo, vsmul(t, d));
+        N = vnorm(vsub(P, c));
+        hit = best;
+        if (sc.mat(hit).opacity > 0.f) {
+          msum = v3(0.f, 0.f, 0.f);
+          li = -1;
+          nextLight = true;
+        } else {
+          afterMatte = true;
+        }
+      }
+    } else {  // kShadow: the query was light li's shadow ray
+      bool blockedL = false;
+      if (best >= 0) {
+        const V3 dist = vsmul(t, qd);
+        blockedL = vdot(dist, dist) < lgap;                 // raytracer.h:299
+      }
+      if (!blockedL) {
+        V3 Lpos, Lcol;
+        sc.light((unsigned)li, Lpos, Lcol);
+        msum = vadd(msum, vsmul(linc / lgap, Lcol));        // raytracer.h:354-360
+      }
+      nextLight = true;
+    }
+
+    if (nextLight) {  // next light with positive incidence (raytracer.h:328-349)
+      const int m = (int)sc.m;
+      bool found = false;
+      while (++li < m) {
+        V3 Lpos, Lcol;
+        sc.light((unsigned)li, Lpos, Lcol);
+        const V3 dist = vsub(Lpos, P);
+        const float gap = vdot(dist, dist);
+        const V3 dir = vsmul(1.f / rtg_sqrtf(gap), dist);
+        const float inc = vdot(N, dir);
+        if (inc > 0.f) {
+          lgap = gap;
+          linc = inc;
+          qo = P;
+          qd = dir;
+          found = true;
+          break;
+        }
+      }
+      if (found) {
+        phase = kShadow;
+      } else {
+        afterMatte = true;
+      }
+    }
+
+    if (afterMatte) {  // raytracer.h:463-539 after calculateMatte
+      const Mat mh = sc.mat(hit);
+      const float op = mh.opacity;
+      const float tr = 1.f - op;
+      V3 colour = v3(0.f, 0.f, 0.f);
+      if (op > 0.f) {
+        V3 tmp = vmul(I, mh.matte);
+        tmp = vsmul(op, tmp);
+        tmp = vmul(msum, tmp);
+        colour = vadd(tmp, colour);
+      }
+      if (tr > 0.f) {
+        const bool leaf = (sp >= S - 1);
+        const Mat mr = sc.mat(rm);
+        V3 cdir = v3(0.f, 0.f, 0.f);
+        float R;
+        const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
+        const float prod = tr * R;
+        V3 rc = vsmul(prod, v3(1.f, 1.f, 1.f));
+        rc = vadd(rc, vsmul(mr.opacity, mh.gloss));
+        rc = vmul(I, rc);
+        const bool sigR = significant(rc);
+        if (!leaf) {
+          Frame& f = st[sp < NF ? sp : NF - 1];
+          f.colour = colour;
+          f.rm = rm;
+          f.flags = sigR ? 2 : 0;
+          if (sigR) {
+            const float perp = 2.f * vdot(d, N);
+            const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
+            f.rd = rd;
+            f.ro = vadd(P, vsmul(0.01f, rd));
+            f.rI = rc;
+          }
+          ++sp;
+          ret = colour;
+          I = vsmul((1.f - R), vsmul(tr, I));
+          qo = P;
+          d = cdir;
+          qd = cdir;
+          rm = tgt;
+          phase = kClosest;
+        } else {
+          const V3 c1 = vadd(colour, colour);
+          ret = sigR ? vadd(c1, c1) : c1;
+          unwind = true;
+        }
+      } else {
+        ret = colour;
+        unwind = true;
+      }
+    }
+
+    if (unwind) {
+      bool descend = false;
+      while (sp > 0) {
+        Frame& f = st[sp - 1 < NF ? sp - 1 : NF - 1];
+        f.colour = vadd(ret, f.colour);
+        ret = f.colour;
+        if ((f.flags & 3) == 2) {
+          f.flags = 1;
+          qo = f.ro; d = f.rd; qd = f.rd; I = f.rI; rm = f.rm;
+          descend = true;
+          break;
+        }
+        --sp;
+      }
+      if (descend) {
+        phase = kClosest;
+      } else {
+        // sample finished: main.cpp:442-445
+        pix = vadd(pix, vsmul(cam.inv, ret));
+        ++s;
+        if (s < nSamples) {
+          const int si = s / cam.nAA, sj = s - si * cam.nAA;
+          const float rx = (pxX + (float)(((float)sj) * cam.st)) * cam.asp;
+          const float ry = (pxY + (float)(((float)si) * cam.st));
+          d = vnorm(v3(rx, ry, cam.zoom));
+          qo = v3(0.f, 0.f, 0.f);
+          qd = d;
+          I = v3(1.f, 1.f, 1.f);
+          rm = (int)sc.n;
+          ret = v3(0.f, 0.f, 0.f);
+          phase = kClosest;
+        } else {
+          phase = kDone;
+        }
+      }
+    }
+  }
+  return pix;
+}
+
 // main.cpp:411-452 for pixel (x, y) of the frame.
 template <int S, class Scene>
 RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {

@@ -26,6 +26,9 @@ struct HostScene {
     r2 = g[3];
     return rtg::v3(g[0], g[1], g[2]);
   }
+  void sphere4(unsigned i, rtg::V3* c, float* r2) const {
+    for (int k = 0; k < 4; ++k) c[k] = sphere(i + k, r2[k]);
+  }
   float contain_r2(unsigned i) const { return crad2[i]; }
   rtg::Mat mat(int i) const {
     const float* p = mats + 8 * i;
@@ -44,16 +47,21 @@ struct HostScene {
   }
 };
 
+int g_variant = 0;
+
 template <int S>
 void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, float* out) {
   for (unsigned x = 0; x < W; ++x) {
-    rtg::V3 p = rtg::shade_pixel<S>(sc, cam, x, y);
+    rtg::V3 p = g_variant == 1 ? rtg::shade_pixel<S>(sc, cam, x, y)
+                               : rtg::shade_pixel_persistent<S>(sc, cam, x, y);
     out[3 * x + 0] = p.x;
     out[3 * x + 1] = p.y;
     out[3 * x + 2] = p.z;
   }
 }
 }  // namespace
+
+extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 
 extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
                                    const rtg_light* lights, unsigned m, unsigned W,

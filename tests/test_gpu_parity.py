@@ -175,3 +175,24 @@ def test_errors_are_returned_not_fatal(R):
     # still usable afterwards
     fb = R.render(sph, lg, 8, 8)
     assert fb.shape == (8, 8, 3)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
+    """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
+    torch = torch_cuda
+    ctx = R.Context(0)
+    ctx.set_variant(variant)
+    for name in ["ref800", "c2", "c3", "c5"]:
+        c = golden["configs"][name]
+        sph, lg = load_scene(name, c["spheres"], c["lights"])
+        sw, sh = c["small"]["W"], c["small"]["H"]
+        want = load_f32(os.path.join(GOLDEN, f"{name}.small.f32"), (sh, sw, 3))
+        ctx.set_scene(sph, lg)
+        out = torch.empty((sh, sw, 3), dtype=torch.float32, device="cuda")
+        ctx.render_device(sw, sh, out.data_ptr(), stack_size=c["stack_size"],
+                          stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert bits_equal(got, want), (name, variant, first_mismatch(got, want))
+    ctx.close()

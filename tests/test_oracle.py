@@ -131,6 +131,13 @@ def hostsim():
     return ctypes.CDLL(so)
 
 
+@pytest.fixture(params=[0, 1], ids=["persistent", "recursive"])
+def variant(request, hostsim):
+    hostsim.hostsim_set_variant(request.param)
+    yield request.param
+    hostsim.hostsim_set_variant(0)
+
+
 def _hostsim_render(hs, sph, lg, W, H, S, aa=3.0, zoom=-4.0, rows=None):
     rows = np.arange(H, dtype=np.uint32) if rows is None else np.asarray(rows, np.uint32)
     out = np.zeros((len(rows), W, 3), np.float32)
@@ -141,7 +148,7 @@ def _hostsim_render(hs, sph, lg, W, H, S, aa=3.0, zoom=-4.0, rows=None):
 
 
 @pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
-def test_kernel_traversal_small_frames(hostsim, golden, name):
+def test_kernel_traversal_small_frames(hostsim, variant, golden, name):
     c = golden["configs"][name]
     sph, lg = load_scene(name, c["spheres"], c["lights"])
     sw, sh = c["small"]["W"], c["small"]["H"]
@@ -150,7 +157,7 @@ def test_kernel_traversal_small_frames(hostsim, golden, name):
     assert bits_equal(got, want), first_mismatch(got, want)
 
 
-def test_kernel_traversal_edge_cases(hostsim, golden):
+def test_kernel_traversal_edge_cases(hostsim, variant, golden):
     for c in golden["cases"]:
         if c["stack_size"] > 12:
             continue  # hostsim instantiates S <= 12
@@ -161,7 +168,7 @@ def test_kernel_traversal_edge_cases(hostsim, golden):
         assert bits_equal(got, want), (c["name"], first_mismatch(got, want))
 
 
-def test_kernel_traversal_random_scenes(hostsim, oracle, rtg):
+def test_kernel_traversal_random_scenes(hostsim, variant, oracle, rtg):
     rng = np.random.default_rng(11)
     for trial in range(40):
         S = int(rng.integers(1, 13))
@@ -175,7 +182,7 @@ def test_kernel_traversal_random_scenes(hostsim, oracle, rtg):
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
 
 
-def test_kernel_traversal_c1_full_frame(hostsim, golden):
+def test_kernel_traversal_c1_full_frame(hostsim, variant, golden):
     """A whole BASELINE config frame through the kernel's traversal (md5)."""
     c = golden["configs"]["c1"]
     sph, lg = load_scene("c1", c["spheres"], c["lights"])

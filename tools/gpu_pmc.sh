@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# tools/gpu_pmc.sh — PMC passes (one counter group per rocprofv3 run, kernel
+# trace only, as MI355X_MICROARCH.md prescribes) over a short bench run.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=$PWD/gpurun_out
+TAG=${TAG:-r01}
+ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+mkdir -p $OUT/pmc_$TAG
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > $OUT/pmc_$TAG/counters_list.txt 2>&1 || true
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" ${EXTRA_GROUPS}; do
+  i=$((i+1))
+  echo "== pass $i: $grp"
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc_$TAG/p$i -o run \
+     -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/pmc_$TAG/p$i.json 2> $OUT/pmc_$TAG/p$i.err || { echo "pass $i failed"; tail -5 $OUT/pmc_$TAG/p$i.err; exit 1; }
+done
+echo "== done"
