@@ -41,7 +41,7 @@ namespace rtg {
 
 constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
 // Materials staged in LDS when the table fits (n+1 records of 32 B).
-constexpr unsigned kLdsMatMax = 1024 + 1;
+constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 
 // Device scene: geometry SoA-ish float4 {x, y, z, r*r}, (r + 1e-6f)^2, the
 // material table (n+1 x 8 floats; [n] = background), lights (m x 6 floats).
@@ -59,6 +59,7 @@ struct DevScene {
   cfloat_p geom;      // n x {x, y, z, r*r}
   cfloat_p crad2;
   MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)
+  const float4* lgeom;  // LDS copy of geom (or the global array when it does not fit)
   cfloat_p lights;
   unsigned n, m;
 
@@ -75,6 +76,12 @@ struct DevScene {
       c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
       r2[k] = g[4 * k + 3];
     }
+  }
+  // Per-lane sphere record (divergent index): from the LDS copy.
+  __device__ __forceinline__ V3 sphere_lane(unsigned i, float& r2) const {
+    const float4 g = lgeom[i];
+    r2 = g.w;
+    return v3(g.x, g.y, g.z);
   }
   __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
   __device__ __forceinline__ Mat mat(int i) const {
@@ -111,33 +118,37 @@ __device__ __forceinline__ float canon_nan(float v) {
   return (v != v) ? __uint_as_float(0xFFC00000u) : v;
 }
 
-template <int S, bool kLdsMats, int kVariant>
+template <int S, bool kLds, int kVariant>
 __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
-  extern __shared__ float lmats[];  // (n+1)*8 floats when kLdsMats
-  typedef typename std::conditional<kLdsMats, const float*, cfloat_p>::type MatPtr;
+  // LDS image when kLds: material table (n+1) x 8 floats, then geometry n x float4.
+  extern __shared__ float4 lds4[];
+  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
   DevScene<MatPtr> sc;
-  if constexpr (kLdsMats) {
+  if constexpr (kLds) {
+    float* lmats = reinterpret_cast<float*>(lds4);
     const unsigned nm = (a.n + 1) * 8;
     for (unsigned i = threadIdx.x; i < nm; i += kBlock) lmats[i] = a.mats[i];
+    float4* lg = lds4 + (a.n + 1) * 2;
+    for (unsigned i = threadIdx.x; i < a.n; i += kBlock)
+      lg[i] = reinterpret_cast<const float4*>(a.geom)[i];
     __syncthreads();
     sc.mats = lmats;
+    sc.lgeom = lg;
   } else {
     sc.mats = (cfloat_p)a.mats;
+    sc.lgeom = reinterpret_cast<const float4*>(a.geom);
   }
-  sc.geom = (cfloat_p)a.geom;
-  sc.crad2 = (cfloat_p)a.crad2;
-  sc.lights = (cfloat_p)a.lights;
-  sc.n = a.n;
-  sc.m = a.m;
-
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned x = blockIdx.x * kTileW + (wave & 1u) * 8u + (lane & 7u);
   const unsigned lr = blockIdx.y * kTileH + (wave >> 1) * 8u + (lane >> 3);
   if (x >= a.W || lr >= a.rowsLocal) return;
   const unsigned gy =
       a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
-  const V3 pix = (kVariant == 1) ? shade_pixel<S>(sc, a.cam, x, gy)
-                                 : shade_pixel_persistent<S>(sc, a.cam, x, gy);
+  V3 pix;
+  if constexpr (kVariant == 0) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
+  else if constexpr (kVariant == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
+  else if constexpr (kVariant == 2) pix = shade_pixel<S, 2>(sc, a.cam, x, gy);
+  else pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
   float* o = a.dst + ((size_t)lr * a.W + x) * 3;
   o[0] = canon_nan(pix.x);
   o[1] = canon_nan(pix.y);
@@ -184,12 +195,23 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 }
 
 typedef void (*TraceFn)(const KernelArgs);
-// variant 0 (default) = persistent state machine (shade_pixel_persistent);
-// variant 1 = per-sample recursion (shade_pixel), kept for A/B measurement.
+// Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
+//   0 (default) persistent state machine + two-pass candidate-mask queries
+//   1 per-sample recursion, one sphere per step (first kernel)
+//   2 per-sample recursion + two-pass candidate-mask queries
+//   3 persistent state machine, four spheres per step
+template <int S, int V>
+static TraceFn trace_fn_v(bool lds) {
+  return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
+}
 template <int S>
 static TraceFn trace_fn(bool lds, int variant) {
-  if (variant == 1) return lds ? trace_kernel<S, true, 1> : trace_kernel<S, false, 1>;
-  return lds ? trace_kernel<S, true, 0> : trace_kernel<S, false, 0>;
+  switch (variant) {
+    case 1: return trace_fn_v<S, 1>(lds);
+    case 2: return trace_fn_v<S, 2>(lds);
+    case 3: return trace_fn_v<S, 3>(lds);
+    default: return trace_fn_v<S, 0>(lds);
+  }
 }
 
 static TraceFn pick_trace(int S, bool lds, int variant) {
@@ -376,7 +398,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.dst = reinterpret_cast<float*>(dstDevice);
   HIP_TRY(hipSetDevice(ctx->device));
   dim3 grid((width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
-  const size_t lds = ldsMats ? (size_t)(ctx->n + 1) * 8 * sizeof(float) : 0;
+  const size_t lds =
+      ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) + (size_t)ctx->n * 16) : 0;
   hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());
   return RTG_OK;

@@ -151,8 +151,14 @@ RTG_HD int primary_container(const Scene& sc, V3 pt) {
   return -1;
 }
 
+// Query strategies (defined below): see query_closest / query_blocked.
+template <int Q, class Scene>
+RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t);
+template <int Q, class Scene>
+RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap);
+
 // raytracer.h:313-367, with the incidence test hoisted ahead of the shadow ray.
-template <class Scene>
+template <int Q, class Scene>
 RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
   V3 sum = v3(0.f, 0.f, 0.f);
   const unsigned m = sc.m;
@@ -164,7 +170,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
     const V3 dir = vsmul(1.f / rtg_sqrtf(gap), dist);  // vnorm(dist)
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
-      if (!blocked(sc, P, dir, gap)) {
+      if (!query_blocked<Q>(sc, P, dir, gap)) {
         const float intensity = incidence / gap;
         sum = vadd(sum, vsmul(intensity, Lcol));
       }
@@ -246,7 +252,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
-template <int S, class Scene>
+template <int S, int Q, class Scene>
 RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   Frame st[NF];
@@ -257,7 +263,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
   for (;;) {
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
-    const int hit = closest_hit(sc, o, d, t);
+    const int hit = query_closest<Q>(sc, o, d, t);
     if (hit < 0) {
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
@@ -272,7 +278,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
       if (op > 0.f) {
         V3 tmp = vmul(I, mh.matte);
         tmp = vsmul(op, tmp);
-        const V3 mc = matte_light(sc, P, N);
+        const V3 mc = matte_light<Q>(sc, P, N);
         tmp = vmul(mc, tmp);
         colour = vadd(tmp, colour);
       }
@@ -399,7 +405,120 @@ RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
   return best;
 }
 
-template <int S, class Scene>
+// Two-pass query (default).  Pass 1 runs over every sphere with a wave-
+// uniform index and no branches: it only evaluates the radicand
+// (raytracer.h:95-104) and sets bit k of a per-lane candidate mask when it is
+// >= 0.  Pass 2 walks each lane's candidates in increasing index order (so the
+// first index still wins ties) and does the expensive part — sqrt, the two
+// divisions, the root selection (raytracer.h:105-138) — with the candidate's
+// record fetched per lane (`sphere_lane`).  Lanes with candidates run pass 2
+// together instead of every sphere's branch running for whichever lanes need
+// it.  The radicand is recomputed with the same operations, so it is the same
+// value.  Spheres are processed in chunks of 32 (one mask word).
+template <class Scene>
+RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, V3 o, V3 d,
+                               float a4) {
+  unsigned mask = 0;
+  unsigned k = 0;
+  for (; k + 4 <= cnt; k += 4) {
+    V3 c[4];
+    float r2[4];
+    sc.sphere4(base + k, c, r2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const V3 disp = vsub(o, c[q]);
+      const float b = 2.0f * vdot(d, disp);
+      const float cc = vdot(disp, disp) - r2[q];
+      const float rad = (b * b) - (a4 * cc);
+      mask |= (rad >= 0.0f) ? (1u << (k + q)) : 0u;
+    }
+  }
+  for (; k < cnt; ++k) {
+    float r2;
+    const V3 c = sc.sphere(base + k, r2);
+    const V3 disp = vsub(o, c);
+    const float b = 2.0f * vdot(d, disp);
+    const float cc = vdot(disp, disp) - r2;
+    const float rad = (b * b) - (a4 * cc);
+    mask |= (rad >= 0.0f) ? (1u << k) : 0u;
+  }
+  return mask;
+}
+
+RTG_HD int lowest_bit(unsigned m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_ctz(m);
+#else
+  return __builtin_ctz(m);
+#endif
+}
+
+template <class Scene>
+RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
+  const float a = vdot(d, d);
+  const float a4 = 4.0f * a;
+  const float den = 2.0f * a;
+  float minT = 1000.f;
+  int best = -1;
+  const unsigned n = sc.n;
+  for (unsigned base = 0; base < n; base += 32) {
+    const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;
+    unsigned mask = candidate_mask(sc, base, cnt, o, d, a4);
+    while (mask) {
+      const unsigned i = base + (unsigned)lowest_bit(mask);
+      mask &= mask - 1;
+      float r2;
+      const V3 c = sc.sphere_lane(i, r2);
+      bool res;
+      const float t = ray_sphere(o, d, c, r2, a4, den, res);
+      if (res && t < minT) { minT = t; best = (int)i; }
+    }
+  }
+  tOut = minT;
+  return best;
+}
+
+// Shadow query with the two-pass scheme; stops at the first blocker.
+template <class Scene>
+RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
+  const float a = vdot(d, d);
+  const float a4 = 4.0f * a;
+  const float den = 2.0f * a;
+  const unsigned n = sc.n;
+  for (unsigned base = 0; base < n; base += 32) {
+    const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;
+    unsigned mask = candidate_mask(sc, base, cnt, o, d, a4);
+    while (mask) {
+      const unsigned i = base + (unsigned)lowest_bit(mask);
+      mask &= mask - 1;
+      float r2;
+      const V3 c = sc.sphere_lane(i, r2);
+      bool res;
+      const float t = ray_sphere(o, d, c, r2, a4, den, res);
+      if (res && t < 1000.f) {
+        const V3 dist = vsmul(t, d);
+        if (vdot(dist, dist) < gap) return true;
+      }
+    }
+  }
+  return false;
+}
+
+// Query strategy selector: 0 = one sphere per step with a branch per sphere,
+// 1 = four spheres per step, 2 = two-pass candidate masks.
+template <int Q, class Scene>
+RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t) {
+  if constexpr (Q == 0) return closest_hit(sc, o, d, t);
+  else if constexpr (Q == 1) return closest_hit4(sc, o, d, t);
+  else return closest_hit_mask(sc, o, d, t);
+}
+template <int Q, class Scene>
+RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap) {
+  if constexpr (Q == 2) return blocked_mask(sc, o, d, gap);
+  else return blocked(sc, o, d, gap);
+}
+
+template <int S, int Q, class Scene>
 RTG_HD V3 shade_pixel_persistent(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   enum : int { kClosest = 0, kShadow = 1, kDone = 2 };
@@ -433,7 +552,7 @@ RTG_HD V3 shade_pixel_persistent(const Scene& sc, const Camera& cam, unsigned x,
 
   while (phase != kDone) {
     float t;
-    const int best = closest_hit4(sc, qo, qd, t);
+    const int best = query_closest<Q>(sc, qo, qd, t);
 
     bool nextLight = false, afterMatte = false, unwind = false;
     if (phase == kClosest) {
@@ -590,7 +709,7 @@ RTG_HD V3 shade_pixel_persistent(const Scene& sc, const Camera& cam, unsigned x,
 }
 
 // main.cpp:411-452 for pixel (x, y) of the frame.
-template <int S, class Scene>
+template <int S, int Q, class Scene>
 RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
   const float pxX = (((float)x - cam.halfW)) * cam.xs;
   const float pxY = (cam.halfH - (float)y) * cam.ys;
@@ -600,7 +719,7 @@ RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y
       const float rx = (pxX + (float)(((float)j) * cam.st)) * cam.asp;
       const float ry = (pxY + (float)(((float)i) * cam.st));
       const V3 dir = vnorm(v3(rx, ry, cam.zoom));
-      V3 c = trace_sample<S>(sc, dir);
+      V3 c = trace_sample<S, Q>(sc, dir);
       c = vsmul(cam.inv, c);
       pix = vadd(pix, c);
     }

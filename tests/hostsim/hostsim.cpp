@@ -26,6 +26,7 @@ struct HostScene {
     r2 = g[3];
     return rtg::v3(g[0], g[1], g[2]);
   }
+  rtg::V3 sphere_lane(unsigned i, float& r2) const { return sphere(i, r2); }
   void sphere4(unsigned i, rtg::V3* c, float* r2) const {
     for (int k = 0; k < 4; ++k) c[k] = sphere(i + k, r2[k]);
   }
@@ -52,8 +53,13 @@ int g_variant = 0;
 template <int S>
 void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, float* out) {
   for (unsigned x = 0; x < W; ++x) {
-    rtg::V3 p = g_variant == 1 ? rtg::shade_pixel<S>(sc, cam, x, y)
-                               : rtg::shade_pixel_persistent<S>(sc, cam, x, y);
+    rtg::V3 p;
+    switch (g_variant) {
+      case 1: p = rtg::shade_pixel<S, 0>(sc, cam, x, y); break;
+      case 2: p = rtg::shade_pixel<S, 2>(sc, cam, x, y); break;
+      case 3: p = rtg::shade_pixel_persistent<S, 1>(sc, cam, x, y); break;
+      default: p = rtg::shade_pixel_persistent<S, 2>(sc, cam, x, y); break;
+    }
     out[3 * x + 0] = p.x;
     out[3 * x + 1] = p.y;
     out[3 * x + 2] = p.z;
