@@ -138,6 +138,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
     sc.mats = (cfloat_p)a.mats;
     sc.lgeom = reinterpret_cast<const float4*>(a.geom);
   }
+  sc.geom = (cfloat_p)a.geom;
+  sc.crad2 = (cfloat_p)a.crad2;
+  sc.lights = (cfloat_p)a.lights;
+  sc.n = a.n;
+  sc.m = a.m;
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned x = blockIdx.x * kTileW + (wave & 1u) * 8u + (lane & 7u);
   const unsigned lr = blockIdx.y * kTileH + (wave >> 1) * 8u + (lane >> 3);
