@@ -111,6 +111,8 @@ def main():
     ap.add_argument("--ab", default="", help="comma list of kernel variants to A/B after the "
                     "timed run (interleaved rounds, kernel time via HIP events)")
     ap.add_argument("--ab-rounds", type=int, default=5)
+    ap.add_argument("--diag", type=int, default=0, help="diagnostic variant (e.g. 102) to run "
+                    "once after timing; reports s_memtime cycle shares per phase")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -184,6 +186,21 @@ def main():
 
     ms_per_step = elapsed / args.steps * 1e3
     mpx = W * H / (elapsed / args.steps) / 1e6
+
+    diag = None
+    if args.diag and world == 1:
+        ctx.set_variant(args.diag)
+        ctx.diag_read(reset=True)
+        ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, stream=sptr)
+        torch.cuda.synchronize()
+        cyc = ctx.diag_read(reset=True)
+        tot = max(cyc[3], 1)
+        diag = {"variant": args.diag, "wave_cycles_total": cyc[3],
+                "share_closest": round(cyc[0] / tot, 4), "share_shadow": round(cyc[1] / tot, 4),
+                "share_refraction": round(cyc[2] / tot, 4),
+                "share_other": round(1 - (cyc[0] + cyc[1] + cyc[2]) / tot, 4)}
+        log("diag", diag)
+        ctx.set_variant(args.variant)
 
     ab = None
     if args.ab and world == 1:
@@ -285,6 +302,7 @@ def main():
         "gpu_vs_cpu": round(mpx / cpu["value"], 1) if cpu else None,
         "parity": parity,
         "ab": ab,
+        "diag": diag,
     }
     print(json.dumps(out), flush=True)
     ctx.close()

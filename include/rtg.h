@@ -132,6 +132,10 @@ typedef struct rtg_launch_opts {
   int reserved[7];
 } rtg_launch_opts;
 int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts);
+/* Diagnostic variants (variant >= 100) sum per-wave s_memtime cycles spent in
+ * {closest-hit queries, shadow queries, refraction, whole pixel} into 8
+ * counters; read (and optionally zero) them.  Zeros for normal variants. */
+int rtg_diag_read(rtg_context* ctx, unsigned long long* out8, int reset);
 
 /* ---- output side ---- */
 /* algebra.h:68-91 on the host. */

@@ -54,8 +54,26 @@ constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 #endif
 typedef const RTG_CONST float* cfloat_p;
 
-template <class MatPtr>
+template <class MatPtr, bool kDiag = false>
 struct DevScene {
+  // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
+  // probe slot, summed per wave and added to KernelArgs::diag at exit.
+  mutable unsigned long long acc[kProbeSlots];
+  mutable unsigned long long t0;
+  __device__ __forceinline__ void probe_begin() const {
+    if constexpr (kDiag) {
+      __builtin_amdgcn_sched_barrier(0);
+      t0 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __device__ __forceinline__ void probe_end(int slot) const {
+    if constexpr (kDiag) {
+      __builtin_amdgcn_sched_barrier(0);
+      acc[slot] += __builtin_amdgcn_s_memtime() - t0;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   cfloat_p geom;      // n x {x, y, z, r*r}
   cfloat_p crad2;
   MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)
@@ -111,6 +129,7 @@ struct KernelArgs {
   unsigned W, rowsLocal, rowBlock, shard, nShards;
   const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
   float* dst;
+  unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
 };
 
 __device__ __forceinline__ float canon_nan(float v) {
@@ -123,7 +142,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   // LDS image when kLds: material table (n+1) x 8 floats, then geometry n x float4.
   extern __shared__ float4 lds4[];
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr> sc;
+  constexpr bool kDiag = kVariant >= 100;
+  constexpr int kBase = kDiag ? kVariant - 100 : kVariant;
+  DevScene<MatPtr, kDiag> sc;
+  if constexpr (kDiag)
+    for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
   if constexpr (kLds) {
     float* lmats = reinterpret_cast<float*>(lds4);
     const unsigned nm = (a.n + 1) * 8;
@@ -150,10 +173,18 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   const unsigned gy =
       a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
   V3 pix;
-  if constexpr (kVariant == 0) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
-  else if constexpr (kVariant == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
-  else if constexpr (kVariant == 2) pix = shade_pixel<S, 2>(sc, a.cam, x, gy);
+  unsigned long long tk0 = 0;
+  if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
+  if constexpr (kBase == 0) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 2) pix = shade_pixel<S, 2>(sc, a.cam, x, gy);
   else pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
+  if constexpr (kDiag) {
+    sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
+    // one wave-level add per slot (values are wave-uniform: s_memtime is scalar)
+    if ((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(__ballot(1)))
+      for (int k = 0; k < kProbeSlots; ++k) atomicAdd(&a.diag[k], sc.acc[k]);
+  }
   float* o = a.dst + ((size_t)lr * a.W + x) * 3;
   o[0] = canon_nan(pix.x);
   o[1] = canon_nan(pix.y);
@@ -212,6 +243,7 @@ static TraceFn trace_fn_v(bool lds) {
 template <int S>
 static TraceFn trace_fn(bool lds, int variant) {
   switch (variant) {
+    case 102: return trace_fn_v<S, 102>(lds);  // diagnostic build of variant 2
     case 1: return trace_fn_v<S, 1>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
@@ -240,6 +272,7 @@ struct rtg_context {
   float* mats = nullptr;
   float* lights = nullptr;
   unsigned* maxScratch = nullptr;
+  unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   rtg_launch_opts opts{};
   bool hasScene = false;
 };
@@ -308,7 +341,22 @@ int rtg_context_destroy(rtg_context* ctx) {
   (void)hipSetDevice(ctx->device);
   free_scene(ctx);
   (void)hipFree(ctx->maxScratch);
+  (void)hipFree(ctx->diag);
   delete ctx;
+  return RTG_OK;
+}
+
+int rtg_diag_read(rtg_context* ctx, unsigned long long* out, int reset) {
+  rtg_clear_error();
+  if (!ctx || !out) return RTG_ERR_INVALID;
+  if (!ctx->diag) {
+    for (int k = 0; k < 8; ++k) out[k] = 0;
+    return RTG_OK;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, ctx->diag, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (reset) HIP_TRY(hipMemset(ctx->diag, 0, 8 * sizeof(unsigned long long)));
   return RTG_OK;
 }
 
@@ -401,6 +449,14 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.nShards = nShards ? nShards : 1;
   a.rowList = rowList;
   a.dst = reinterpret_cast<float*>(dstDevice);
+  a.diag = nullptr;
+  if (ctx->opts.variant >= 100) {
+    if (!ctx->diag) {
+      HIP_TRY(hipMalloc(&ctx->diag, 8 * sizeof(unsigned long long)));
+      HIP_TRY(hipMemset(ctx->diag, 0, 8 * sizeof(unsigned long long)));
+    }
+    a.diag = ctx->diag;
+  }
   HIP_TRY(hipSetDevice(ctx->device));
   dim3 grid((width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
   const size_t lds =

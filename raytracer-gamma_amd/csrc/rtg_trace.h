@@ -70,6 +70,10 @@ struct Camera {
 // material {0,0,0, 0,0,0, opacity 0, n 1.0} (raytracer.h:694-697).
 struct Mat { V3 matte, gloss; float opacity, refr; };
 
+// Diagnostic probe slots (scenes without probes implement them as no-ops).
+enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
+             kProbeSlots = 4 };
+
 // One ancestor frame.
 struct Frame {
   V3 colour;
@@ -79,19 +83,59 @@ struct Frame {
 };
 
 // ---------------------------------------------------------------------------
+// Quotient of the root test.  The reference divides twice per candidate
+// sphere, (-b +- root) / (2a) (raytracer.h:112-116); both share the
+// denominator, so the kernel takes y = 1/den once per ray (correctly rounded)
+// and forms each quotient as q1 = fl(a*y) refined twice with FMA residuals
+// (Markstein: q1 is faithful and y is within half an ulp of 1/den, so the
+// second residual is exact and the result is the correctly rounded quotient).
+// A quotient is only ever used through `u > 1e-5f && u < 10000.f` and its
+// exact value when that holds; tests/fpcheck/markstein_check.c verifies that
+// property over 1e9 operand pairs (incl. subnormal numerators and values at
+// both thresholds) for den in [2^-60, 2^60].  Outside that range the correctly
+// rounded division is used.
+struct RayQ {
+  V3 o, d;
+  float a4, den, y;
+  bool fast;
+};
+
+RTG_HD RayQ make_query(V3 o, V3 d) {
+  RayQ q;
+  q.o = o;
+  q.d = d;
+  const float a = vdot(d, d);
+  q.a4 = 4.0f * a;
+  q.den = 2.0f * a;
+  q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
+  q.y = 1.0f / q.den;
+  return q;
+}
+
+RTG_HD float quot(float x, const RayQ& q) {
+  if (q.fast) {
+    const float q0 = x * q.y;
+    const float r0 = fmaf(-q0, q.den, x);
+    const float q1 = fmaf(r0, q.y, q0);
+    const float r1 = fmaf(-q1, q.den, x);
+    return fmaf(r1, q.y, q1);
+  }
+  return x / q.den;
+}
+
 // Per-sphere ray test, raytracer.h:81-141.  Returns the smallest root in
-// (1e-5, 10000) or 10000 when none (`res` tells).  a4 = 4.0f*a, den = 2.0f*a.
-RTG_HD float ray_sphere(V3 o, V3 d, V3 c, float r2, float a4, float den, bool& res) {
-  V3 disp = vsub(o, c);
-  const float b = 2.0f * vdot(d, disp);
+// (1e-5, 10000) or 10000 when none (`res` tells).
+RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
+  V3 disp = vsub(q.o, c);
+  const float b = 2.0f * vdot(q.d, disp);
   const float cc = vdot(disp, disp) - r2;
-  const float radicand = (b * b) - (a4 * cc);
+  const float radicand = (b * b) - (q.a4 * cc);
   float sm = 10000.f;
   res = false;
   if (radicand >= 0.0f) {
     const float root = rtg_sqrtf(radicand);
-    const float u0 = (-b + root) / den;
-    const float u1 = (-b - root) / den;
+    const float u0 = quot(-b + root, q);
+    const float u1 = quot(-b - root, q);
     if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
     if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
   }
@@ -101,9 +145,7 @@ RTG_HD float ray_sphere(V3 o, V3 d, V3 c, float r2, float a4, float den, bool& r
 // Closest hit, raytracer.h:145-194 (first index wins ties; minT starts 1000).
 template <class Scene>
 RTG_HD int closest_hit(const Scene& sc, V3 o, V3 d, float& tOut) {
-  const float a = vdot(d, d);
-  const float a4 = 4.0f * a;
-  const float den = 2.0f * a;
+  const RayQ q = make_query(o, d);
   float minT = 1000.f;
   int best = -1;
   const unsigned n = sc.n;
@@ -111,7 +153,7 @@ RTG_HD int closest_hit(const Scene& sc, V3 o, V3 d, float& tOut) {
     float r2;
     V3 c = sc.sphere(i, r2);
     bool res;
-    float t = ray_sphere(o, d, c, r2, a4, den, res);
+    float t = ray_sphere(q, c, r2, res);
     if (res && t < minT) { minT = t; best = (int)i; }
   }
   tOut = minT;
@@ -121,15 +163,13 @@ RTG_HD int closest_hit(const Scene& sc, V3 o, V3 d, float& tOut) {
 // Shadow query, raytracer.h:272-309 (see header note for the early exit).
 template <class Scene>
 RTG_HD bool blocked(const Scene& sc, V3 o, V3 d, float gap) {
-  const float a = vdot(d, d);
-  const float a4 = 4.0f * a;
-  const float den = 2.0f * a;
+  const RayQ q = make_query(o, d);
   const unsigned n = sc.n;
   for (unsigned i = 0; i < n; ++i) {
     float r2;
     V3 c = sc.sphere(i, r2);
     bool res;
-    float t = ray_sphere(o, d, c, r2, a4, den, res);
+    float t = ray_sphere(q, c, r2, res);
     if (res && t < 1000.f) {
       V3 dist = vsmul(t, d);
       if (vdot(dist, dist) < gap) return true;
@@ -170,7 +210,10 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
     const V3 dir = vsmul(1.f / rtg_sqrtf(gap), dist);  // vnorm(dist)
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
-      if (!query_blocked<Q>(sc, P, dir, gap)) {
+      sc.probe_begin();
+      const bool blk = query_blocked<Q>(sc, P, dir, gap);
+      sc.probe_end(kProbeShadow);
+      if (!blk) {
         const float intensity = incidence / gap;
         sum = vadd(sum, vsmul(intensity, Lcol));
       }
@@ -263,7 +306,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
   for (;;) {
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
+    sc.probe_begin();
     const int hit = query_closest<Q>(sc, o, d, t);
+    sc.probe_end(kProbeClosest);
     if (hit < 0) {
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
@@ -287,7 +332,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
         const Mat mr = sc.mat(rm);
         V3 cdir;
         float R;
+        sc.probe_begin();
         const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
+        sc.probe_end(kProbeRefraction);
         // stage-1 reflection colour, raytracer.h:563-578
         const float prod = tr * R;
         V3 rc = vsmul(prod, v3(1.f, 1.f, 1.f));
@@ -361,9 +408,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
 // when the scene supports it), first index wins ties: raytracer.h:145-194.
 template <class Scene>
 RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
-  const float a = vdot(d, d);
-  const float a4 = 4.0f * a;
-  const float den = 2.0f * a;
+  const RayQ q = make_query(o, d);
+  const float a4 = q.a4;
   float minT = 1000.f;
   int best = -1;
   const unsigned n = sc.n;
@@ -384,8 +430,8 @@ RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
     for (int k = 0; k < 4; ++k) {
       if (rad[k] >= 0.0f) {
         const float root = rtg_sqrtf(rad[k]);
-        const float u0 = (-b[k] + root) / den;
-        const float u1 = (-b[k] - root) / den;
+        const float u0 = quot(-b[k] + root, q);
+        const float u1 = quot(-b[k] - root, q);
         float sm = 10000.f;
         bool res = false;
         if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
@@ -398,7 +444,7 @@ RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
     float r2;
     V3 c = sc.sphere(i, r2);
     bool res;
-    float t = ray_sphere(o, d, c, r2, a4, den, res);
+    float t = ray_sphere(q, c, r2, res);
     if (res && t < minT) { minT = t; best = (int)i; }
   }
   tOut = minT;
@@ -455,22 +501,20 @@ RTG_HD int lowest_bit(unsigned m) {
 
 template <class Scene>
 RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
-  const float a = vdot(d, d);
-  const float a4 = 4.0f * a;
-  const float den = 2.0f * a;
+  const RayQ q = make_query(o, d);
   float minT = 1000.f;
   int best = -1;
   const unsigned n = sc.n;
   for (unsigned base = 0; base < n; base += 32) {
     const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;
-    unsigned mask = candidate_mask(sc, base, cnt, o, d, a4);
+    unsigned mask = candidate_mask(sc, base, cnt, o, d, q.a4);
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;
-      const float t = ray_sphere(o, d, c, r2, a4, den, res);
+      const float t = ray_sphere(q, c, r2, res);
       if (res && t < minT) { minT = t; best = (int)i; }
     }
   }
@@ -481,20 +525,18 @@ RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
 // Shadow query with the two-pass scheme; stops at the first blocker.
 template <class Scene>
 RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
-  const float a = vdot(d, d);
-  const float a4 = 4.0f * a;
-  const float den = 2.0f * a;
+  const RayQ q = make_query(o, d);
   const unsigned n = sc.n;
   for (unsigned base = 0; base < n; base += 32) {
     const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;
-    unsigned mask = candidate_mask(sc, base, cnt, o, d, a4);
+    unsigned mask = candidate_mask(sc, base, cnt, o, d, q.a4);
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;
-      const float t = ray_sphere(o, d, c, r2, a4, den, res);
+      const float t = ray_sphere(q, c, r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, d);
         if (vdot(dist, dist) < gap) return true;

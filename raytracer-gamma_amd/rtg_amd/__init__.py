@@ -53,7 +53,7 @@ EXPORTED = [
     "rtg_last_error", "rtg_abi_version", "rtg_device_count", "rtg_device_info",
     "rtg_render", "rtg_context_create", "rtg_context_destroy", "rtg_context_set_scene",
     "rtg_shard_rows", "rtg_shard_global_row", "rtg_render_device", "rtg_render_rows_device",
-    "rtg_render_rows", "rtg_set_launch_opts",
+    "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read",
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate",
 ]
@@ -89,6 +89,7 @@ def lib() -> ctypes.CDLL:
         L.rtg_render_rows_device.argtypes = [vp, u, u, f, f, i, vp, u, vp, vp]
         L.rtg_render_rows.argtypes = [i, vp, u, vp, u, u, u, f, f, i, vp, u, vp]
         L.rtg_set_launch_opts.argtypes = [vp, vp]
+        L.rtg_diag_read.argtypes = [vp, vp, i]
         L.rtg_max_colour.argtypes = [vp, sz]
         L.rtg_max_colour.restype = f
         L.rtg_max_colour_device.argtypes = [vp, vp, sz, vp, vp]
@@ -250,6 +251,12 @@ class Context:
         opts = (ctypes.c_int * 8)(variant, 0, 0, 0, 0, 0, 0, 0)
         _check(lib().rtg_set_launch_opts(self._h, ctypes.cast(opts, ctypes.c_void_p)),
                "rtg_set_launch_opts")
+
+    def diag_read(self, reset: bool = True):
+        out = (ctypes.c_ulonglong * 8)()
+        _check(lib().rtg_diag_read(self._h, ctypes.cast(out, ctypes.c_void_p), int(reset)),
+               "rtg_diag_read")
+        return [int(v) for v in out]
 
     def render_device(self, width, height, dst_ptr: int, zoom=-4.0, alias_factor=3.0,
                       stack_size=6, row_block=16, shard=0, n_shards=1, stream: int = 0):
