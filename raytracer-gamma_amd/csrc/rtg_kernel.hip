@@ -175,10 +175,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   V3 pix;
   unsigned long long tk0 = 0;
   if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
-  if constexpr (kBase == 0) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
+  if constexpr (kBase == 0) pix = shade_pixel<S, 2>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
-  else if constexpr (kBase == 2) pix = shade_pixel<S, 2>(sc, a.cam, x, gy);
-  else pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 2) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 3) pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
+  else pix = shade_pixel_nodes<S, 2>(sc, a.cam, x, gy);
   if constexpr (kDiag) {
     sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
     // one wave-level add per slot (values are wave-uniform: s_memtime is scalar)
@@ -232,10 +233,12 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 
 typedef void (*TraceFn)(const KernelArgs);
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
-//   0 (default) persistent state machine + two-pass candidate-mask queries
+//   0 (default) per-sample recursion + two-pass candidate-mask queries
 //   1 per-sample recursion, one sphere per step (first kernel)
-//   2 per-sample recursion + two-pass candidate-mask queries
-//   3 persistent state machine, four spheres per step
+//   2 one-query-per-iteration state machine + candidate masks
+//   3 one-query-per-iteration state machine, four spheres per step
+//   4 node-persistent: samples chained in one node loop + candidate masks
+//   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -243,8 +246,10 @@ static TraceFn trace_fn_v(bool lds) {
 template <int S>
 static TraceFn trace_fn(bool lds, int variant) {
   switch (variant) {
-    case 102: return trace_fn_v<S, 102>(lds);  // diagnostic build of variant 2
+    case 100: return trace_fn_v<S, 100>(lds);
+    case 104: return trace_fn_v<S, 104>(lds);
     case 1: return trace_fn_v<S, 1>(lds);
+    case 4: return trace_fn_v<S, 4>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
     default: return trace_fn_v<S, 0>(lds);

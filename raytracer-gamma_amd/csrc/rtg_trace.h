@@ -750,6 +750,123 @@ RTG_HD V3 shade_pixel_persistent(const Scene& sc, const Camera& cam, unsigned x,
   return pix;
 }
 
+// v4: node-persistent.  Same node step as trace_sample (one whole node per
+// iteration: closest hit, matte with its shadow rays, refraction, push), but
+// the 9 samples of the pixel are chained inside ONE loop, so a lane whose
+// sample tree is finished starts its next sample's primary ray at the next
+// iteration instead of idling until the deepest tree of the wave is done.
+template <int S, int Q, class Scene>
+RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
+  constexpr int NF = (S > 1) ? (S - 1) : 1;
+  const float pxX = (((float)x - cam.halfW)) * cam.xs;
+  const float pxY = (cam.halfH - (float)y) * cam.ys;
+  const int nSamples = cam.nAA * cam.nAA;
+  V3 pix = v3(0.f, 0.f, 0.f);
+  if (nSamples == 0) return pix;
+  Frame st[NF];
+  int sp = 0;
+  int s = 0;
+  V3 ret = v3(0.f, 0.f, 0.f);
+  V3 o = v3(0.f, 0.f, 0.f), I = v3(1.f, 1.f, 1.f), d;
+  int rm = (int)sc.n;
+  {
+    const float rx = (pxX + (float)(((float)0) * cam.st)) * cam.asp;
+    const float ry = (pxY + (float)(((float)0) * cam.st));
+    d = vnorm(v3(rx, ry, cam.zoom));
+  }
+  for (;;) {
+    float t;
+    sc.probe_begin();
+    const int hit = query_closest<Q>(sc, o, d, t);
+    sc.probe_end(kProbeClosest);
+    bool descendNow = false;
+    if (hit < 0) {
+      ret = vmul(I, sc.mat(rm).matte);
+    } else if (significant(I)) {
+      float r2unused;
+      const V3 c = sc.sphere((unsigned)hit, r2unused);
+      const V3 P = vadd(o, vsmul(t, d));
+      const V3 N = vnorm(vsub(P, c));
+      const Mat mh = sc.mat(hit);
+      const float op = mh.opacity;
+      const float tr = 1.f - op;
+      V3 colour = v3(0.f, 0.f, 0.f);
+      if (op > 0.f) {
+        V3 tmp = vmul(I, mh.matte);
+        tmp = vsmul(op, tmp);
+        const V3 mc = matte_light<Q>(sc, P, N);
+        tmp = vmul(mc, tmp);
+        colour = vadd(tmp, colour);
+      }
+      if (tr > 0.f) {
+        const bool leaf = (sp >= S - 1);
+        const Mat mr = sc.mat(rm);
+        V3 cdir;
+        float R;
+        sc.probe_begin();
+        const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
+        sc.probe_end(kProbeRefraction);
+        const float prod = tr * R;
+        V3 rc = vsmul(prod, v3(1.f, 1.f, 1.f));
+        rc = vadd(rc, vsmul(mr.opacity, mh.gloss));
+        rc = vmul(I, rc);
+        const bool sigR = significant(rc);
+        if (!leaf) {
+          Frame& f = st[sp < NF ? sp : NF - 1];
+          f.colour = colour;
+          f.rm = rm;
+          f.flags = sigR ? 2 : 0;
+          if (sigR) {
+            const float perp = 2.f * vdot(d, N);
+            const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
+            f.rd = rd;
+            f.ro = vadd(P, vsmul(0.01f, rd));
+            f.rI = rc;
+          }
+          ++sp;
+          ret = colour;
+          I = vsmul((1.f - R), vsmul(tr, I));
+          o = P;
+          d = cdir;
+          rm = tgt;
+          descendNow = true;
+        } else {
+          const V3 c1 = vadd(colour, colour);
+          ret = sigR ? vadd(c1, c1) : c1;
+        }
+      } else {
+        ret = colour;
+      }
+    }
+    if (descendNow) continue;
+    bool descend = false;
+    while (sp > 0) {
+      Frame& f = st[sp - 1 < NF ? sp - 1 : NF - 1];
+      f.colour = vadd(ret, f.colour);
+      ret = f.colour;
+      if ((f.flags & 3) == 2) {
+        f.flags = 1;
+        o = f.ro; d = f.rd; I = f.rI; rm = f.rm;
+        descend = true;
+        break;
+      }
+      --sp;
+    }
+    if (descend) continue;
+    pix = vadd(pix, vsmul(cam.inv, ret));   // main.cpp:442-445
+    if (++s >= nSamples) break;
+    const int si = s / cam.nAA, sj = s - si * cam.nAA;
+    const float rx = (pxX + (float)(((float)sj) * cam.st)) * cam.asp;
+    const float ry = (pxY + (float)(((float)si) * cam.st));
+    d = vnorm(v3(rx, ry, cam.zoom));
+    o = v3(0.f, 0.f, 0.f);
+    I = v3(1.f, 1.f, 1.f);
+    rm = (int)sc.n;
+    ret = v3(0.f, 0.f, 0.f);
+  }
+  return pix;
+}
+
 // main.cpp:411-452 for pixel (x, y) of the frame.
 template <int S, int Q, class Scene>
 RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {

@@ -58,9 +58,10 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
     rtg::V3 p;
     switch (g_variant) {
       case 1: p = rtg::shade_pixel<S, 0>(sc, cam, x, y); break;
-      case 2: p = rtg::shade_pixel<S, 2>(sc, cam, x, y); break;
+      case 2: p = rtg::shade_pixel_persistent<S, 2>(sc, cam, x, y); break;
       case 3: p = rtg::shade_pixel_persistent<S, 1>(sc, cam, x, y); break;
-      default: p = rtg::shade_pixel_persistent<S, 2>(sc, cam, x, y); break;
+      case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
+      default: p = rtg::shade_pixel<S, 2>(sc, cam, x, y); break;
     }
     out[3 * x + 0] = p.x;
     out[3 * x + 1] = p.y;
