@@ -195,10 +195,13 @@ def main():
         torch.cuda.synchronize()
         cyc = ctx.diag_read(reset=True)
         tot = max(cyc[3], 1)
-        diag = {"variant": args.diag, "wave_cycles_total": cyc[3],
-                "share_closest": round(cyc[0] / tot, 4), "share_shadow": round(cyc[1] / tot, 4),
-                "share_refraction": round(cyc[2] / tot, 4),
-                "share_other": round(1 - (cyc[0] + cyc[1] + cyc[2]) / tot, 4)}
+        names = ["closest", "shadow", "refraction", "total", "matte", "push", "unwind", "shade"]
+        diag = {"variant": args.diag, "wave_cycles_total": cyc[3]}
+        for k, nm in enumerate(names):
+            if k != 3:
+                diag["share_" + nm] = round(cyc[k] / tot, 4)
+        diag["share_outside_closest_shade_unwind"] = round(
+            1 - (cyc[0] + cyc[7] + cyc[6]) / tot, 4)
         log("diag", diag)
         ctx.set_variant(args.variant)
 

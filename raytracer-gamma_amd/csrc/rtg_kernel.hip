@@ -59,18 +59,18 @@ struct DevScene {
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
   mutable unsigned long long acc[kProbeSlots];
-  mutable unsigned long long t0;
-  __device__ __forceinline__ void probe_begin() const {
+  mutable unsigned long long t0[kProbeSlots];
+  __device__ __forceinline__ void probe_begin(int slot) const {
     if constexpr (kDiag) {
       __builtin_amdgcn_sched_barrier(0);
-      t0 = __builtin_amdgcn_s_memtime();
+      t0[slot] = __builtin_amdgcn_s_memtime();
       __builtin_amdgcn_sched_barrier(0);
     }
   }
   __device__ __forceinline__ void probe_end(int slot) const {
     if constexpr (kDiag) {
       __builtin_amdgcn_sched_barrier(0);
-      acc[slot] += __builtin_amdgcn_s_memtime() - t0;
+      acc[slot] += __builtin_amdgcn_s_memtime() - t0[slot];
       __builtin_amdgcn_sched_barrier(0);
     }
   }

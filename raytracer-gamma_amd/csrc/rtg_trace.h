@@ -72,7 +72,8 @@ struct Mat { V3 matte, gloss; float opacity, refr; };
 
 // Diagnostic probe slots (scenes without probes implement them as no-ops).
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
-             kProbeSlots = 4 };
+             kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
+             kProbeSlots = 8 };
 
 // One ancestor frame.
 struct Frame {
@@ -210,7 +211,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
     const V3 dir = vsmul(1.f / rtg_sqrtf(gap), dist);  // vnorm(dist)
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
-      sc.probe_begin();
+      sc.probe_begin(kProbeShadow);
       const bool blk = query_blocked<Q>(sc, P, dir, gap);
       sc.probe_end(kProbeShadow);
       if (!blk) {
@@ -306,9 +307,10 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
   for (;;) {
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
-    sc.probe_begin();
+    sc.probe_begin(kProbeClosest);
     const int hit = query_closest<Q>(sc, o, d, t);
     sc.probe_end(kProbeClosest);
+    sc.probe_begin(kProbeShade);
     if (hit < 0) {
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
@@ -323,7 +325,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
       if (op > 0.f) {
         V3 tmp = vmul(I, mh.matte);
         tmp = vsmul(op, tmp);
+        sc.probe_begin(kProbeMatte);
         const V3 mc = matte_light<Q>(sc, P, N);
+        sc.probe_end(kProbeMatte);
         tmp = vmul(mc, tmp);
         colour = vadd(tmp, colour);
       }
@@ -332,7 +336,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
         const Mat mr = sc.mat(rm);
         V3 cdir;
         float R;
-        sc.probe_begin();
+        sc.probe_begin(kProbeRefraction);
         const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
         sc.probe_end(kProbeRefraction);
         // stage-1 reflection colour, raytracer.h:563-578
@@ -342,6 +346,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
         rc = vmul(I, rc);
         const bool sigR = significant(rc);
         if (!leaf) {
+          sc.probe_begin(kProbePush);
           Frame& f = st[sp < NF ? sp : NF - 1];
           f.colour = colour;
           f.rm = rm;
@@ -361,6 +366,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
           o = P;
           d = cdir;
           rm = tgt;
+          sc.probe_end(kProbePush);
+          sc.probe_end(kProbeShade);
           continue;
         }
         // Leaf: both children dropped by the full stack.
@@ -371,8 +378,10 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
       }
     }
     // else: hit but insignificant intensity -> ret unchanged (stale)
+    sc.probe_end(kProbeShade);
 
     // ---------------- unwind (stages 1 and 2) ----------------
+    sc.probe_begin(kProbeUnwind);
     bool descend = false;
     while (sp > 0) {
       Frame& f = st[sp - 1 < NF ? sp - 1 : NF - 1];
@@ -386,6 +395,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
       }
       --sp;
     }
+    sc.probe_end(kProbeUnwind);
     if (!descend) return ret;
   }
 }
@@ -776,7 +786,7 @@ RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsi
   }
   for (;;) {
     float t;
-    sc.probe_begin();
+    sc.probe_begin(kProbeClosest);
     const int hit = query_closest<Q>(sc, o, d, t);
     sc.probe_end(kProbeClosest);
     bool descendNow = false;
@@ -803,7 +813,7 @@ RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsi
         const Mat mr = sc.mat(rm);
         V3 cdir;
         float R;
-        sc.probe_begin();
+        sc.probe_begin(kProbeRefraction);
         const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
         sc.probe_end(kProbeRefraction);
         const float prod = tr * R;

@@ -27,7 +27,7 @@ struct HostScene {
     return rtg::v3(g[0], g[1], g[2]);
   }
   rtg::V3 sphere_lane(unsigned i, float& r2) const { return sphere(i, r2); }
-  void probe_begin() const {}
+  void probe_begin(int) const {}
   void probe_end(int) const {}
   void sphere4(unsigned i, rtg::V3* c, float* r2) const {
     for (int k = 0; k < 4; ++k) c[k] = sphere(i + k, r2[k]);

@@ -10,7 +10,9 @@ mkdir -p $OUT/pmc_$TAG
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $OUT/pmc_$TAG/counters_list.txt 2>&1 || true
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" ${EXTRA_GROUPS}; do
+GROUPS=${GROUPS:-"FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"}
+IFS='|' read -ra GRPS <<< "$GROUPS"
+for grp in "${GRPS[@]}"; do
   i=$((i+1))
   echo "== pass $i: $grp"
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc_$TAG/p$i -o run \
