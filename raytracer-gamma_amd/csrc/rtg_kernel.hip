@@ -54,8 +54,18 @@ constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 #endif
 typedef const RTG_CONST float* cfloat_p;
 
+// Per-lane frame colours in LDS: level lv of thread t at lfr[lv * kBlock + t]
+// (16-byte records, so a wave's ds_read_b128 covers 1 KiB contiguously and is
+// bank-conflict free).
+struct LdsFrames {
+  FrameC* base;  // already offset by threadIdx.x
+  __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kBlock]; }
+};
+
 template <class MatPtr, bool kDiag = false>
 struct DevScene {
+  FrameC* lfr;
+  __device__ __forceinline__ LdsFrames frames() const { return LdsFrames{lfr}; }
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
   mutable unsigned long long acc[kProbeSlots];
@@ -139,19 +149,23 @@ __device__ __forceinline__ float canon_nan(float v) {
 
 template <int S, bool kLds, int kVariant>
 __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
-  // LDS image when kLds: material table (n+1) x 8 floats, then geometry n x float4.
+  // LDS image: per-lane frame colours ((S-1) x kBlock x 16 B), then, when
+  // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
   extern __shared__ float4 lds4[];
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
   constexpr bool kDiag = kVariant >= 100;
   constexpr int kBase = kDiag ? kVariant - 100 : kVariant;
+  constexpr int NF = (S > 1) ? (S - 1) : 1;
   DevScene<MatPtr, kDiag> sc;
   if constexpr (kDiag)
     for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
+  sc.lfr = reinterpret_cast<FrameC*>(lds4) + threadIdx.x;
+  float4* sceneLds = lds4 + NF * kBlock;
   if constexpr (kLds) {
-    float* lmats = reinterpret_cast<float*>(lds4);
+    float* lmats = reinterpret_cast<float*>(sceneLds);
     const unsigned nm = (a.n + 1) * 8;
     for (unsigned i = threadIdx.x; i < nm; i += kBlock) lmats[i] = a.mats[i];
-    float4* lg = lds4 + (a.n + 1) * 2;
+    float4* lg = sceneLds + (a.n + 1) * 2;
     for (unsigned i = threadIdx.x; i < a.n; i += kBlock)
       lg[i] = reinterpret_cast<const float4*>(a.geom)[i];
     __syncthreads();
@@ -175,7 +189,8 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   V3 pix;
   unsigned long long tk0 = 0;
   if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
-  if constexpr (kBase == 0) pix = shade_pixel<S, 2>(sc, a.cam, x, gy);
+  if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
   else if constexpr (kBase == 2) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
   else if constexpr (kBase == 3) pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
@@ -238,6 +253,7 @@ typedef void (*TraceFn)(const KernelArgs);
 //   2 one-query-per-iteration state machine + candidate masks
 //   3 one-query-per-iteration state machine, four spheres per step
 //   4 node-persistent: samples chained in one node loop + candidate masks
+//   5 as 0 but frame colours in private memory instead of LDS
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
@@ -250,6 +266,7 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 104: return trace_fn_v<S, 104>(lds);
     case 1: return trace_fn_v<S, 1>(lds);
     case 4: return trace_fn_v<S, 4>(lds);
+    case 5: return trace_fn_v<S, 5>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
     default: return trace_fn_v<S, 0>(lds);
@@ -464,8 +481,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   }
   HIP_TRY(hipSetDevice(ctx->device));
   dim3 grid((width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
-  const size_t lds =
-      ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) + (size_t)ctx->n * 16) : 0;
+  const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * kBlock * 16;
+  const size_t lds = frameLds + (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) +
+                                            (size_t)ctx->n * 16)
+                                         : 0);
   hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());
   return RTG_OK;

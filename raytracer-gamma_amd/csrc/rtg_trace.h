@@ -75,6 +75,23 @@ enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTo
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
 
+// Split frame used by trace_sample: the part every unwind step touches
+// (colour, stage flags, refractive material) is 16 bytes and can live in LDS;
+// the pre-computed reflection ray is only read when that child is traced.
+struct FrameC {
+  float cx, cy, cz;
+  unsigned meta;  // rm << 2 | flags (bit0: stage 2, bit1: reflection child significant)
+};
+struct FrameR { V3 ro, rd, rI; };
+
+// Local (private-memory) storage of the colour part, used when the scene does
+// not provide per-lane LDS frames.
+template <int NF>
+struct LocalFrames {
+  FrameC f[NF];
+  RTG_HD FrameC& operator()(int lv) { return f[lv]; }
+};
+
 // One ancestor frame.
 struct Frame {
   V3 colour;
@@ -296,10 +313,10 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
-template <int S, int Q, class Scene>
-RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
+template <int S, int Q, class Scene, class FStore>
+RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
-  Frame st[NF];
+  FrameR fr[NF];                        // reflection child rays (private memory)
   int sp = 0;                           // == level of the node being processed
   V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
@@ -347,17 +364,17 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
         const bool sigR = significant(rc);
         if (!leaf) {
           sc.probe_begin(kProbePush);
-          Frame& f = st[sp < NF ? sp : NF - 1];
-          f.colour = colour;
-          f.rm = rm;
-          f.flags = sigR ? 2 : 0;
+          const int lv = sp < NF ? sp : NF - 1;
+          FrameC& f = fc(lv);
+          f.cx = colour.x; f.cy = colour.y; f.cz = colour.z;
+          f.meta = ((unsigned)rm << 2) | (sigR ? 2u : 0u);
           if (sigR) {
             // calculateReflection, raytracer.h:817-842
             const float perp = 2.f * vdot(d, N);
             const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
-            f.rd = rd;
-            f.ro = vadd(P, vsmul(0.01f, rd));
-            f.rI = rc;
+            fr[lv].rd = rd;
+            fr[lv].ro = vadd(P, vsmul(0.01f, rd));
+            fr[lv].rI = rc;
           }
           ++sp;
           ret = colour;                                       // :538
@@ -384,12 +401,14 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0) {
     sc.probe_begin(kProbeUnwind);
     bool descend = false;
     while (sp > 0) {
-      Frame& f = st[sp - 1 < NF ? sp - 1 : NF - 1];
-      f.colour = vadd(ret, f.colour);                         // :553 / :622
-      ret = f.colour;                                         // :617 / :626
-      if ((f.flags & 3) == 2) {                               // stage 1, reflection
-        f.flags = 1;                                          // -> stage 2
-        o = f.ro; d = f.rd; I = f.rI; rm = f.rm;
+      const int lv = sp - 1 < NF ? sp - 1 : NF - 1;
+      FrameC& f = fc(lv);
+      const V3 fcol = vadd(ret, v3(f.cx, f.cy, f.cz));        // :553 / :622
+      ret = fcol;                                             // :617 / :626
+      if ((f.meta & 3u) == 2u) {                              // stage 1, reflection
+        f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
+        f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
+        o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 2);
         descend = true;
         break;
       }
@@ -878,8 +897,10 @@ RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsi
 }
 
 // main.cpp:411-452 for pixel (x, y) of the frame.
-template <int S, int Q, class Scene>
+template <int S, int Q, bool kSceneFrames = false, class Scene>
 RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
+  constexpr int NF = (S > 1) ? (S - 1) : 1;
+  LocalFrames<NF> local;
   const float pxX = (((float)x - cam.halfW)) * cam.xs;
   const float pxY = (cam.halfH - (float)y) * cam.ys;
   V3 pix = v3(0.f, 0.f, 0.f);
@@ -888,7 +909,9 @@ RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y
       const float rx = (pxX + (float)(((float)j) * cam.st)) * cam.asp;
       const float ry = (pxY + (float)(((float)i) * cam.st));
       const V3 dir = vnorm(v3(rx, ry, cam.zoom));
-      V3 c = trace_sample<S, Q>(sc, dir);
+      V3 c;
+      if constexpr (kSceneFrames) c = trace_sample<S, Q>(sc, dir, sc.frames());
+      else c = trace_sample<S, Q>(sc, dir, local);
       c = vsmul(cam.inv, c);
       pix = vadd(pix, c);
     }

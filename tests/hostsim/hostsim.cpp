@@ -28,6 +28,12 @@ struct HostScene {
   }
   rtg::V3 sphere_lane(unsigned i, float& r2) const { return sphere(i, r2); }
   void probe_begin(int) const {}
+  struct Frames {
+    rtg::FrameC* f;
+    rtg::FrameC& operator()(int lv) const { return f[lv]; }
+  };
+  mutable rtg::FrameC fr[16];
+  Frames frames() const { return Frames{fr}; }
   void probe_end(int) const {}
   void sphere4(unsigned i, rtg::V3* c, float* r2) const {
     for (int k = 0; k < 4; ++k) c[k] = sphere(i + k, r2[k]);
@@ -61,7 +67,8 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 2: p = rtg::shade_pixel_persistent<S, 2>(sc, cam, x, y); break;
       case 3: p = rtg::shade_pixel_persistent<S, 1>(sc, cam, x, y); break;
       case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
-      default: p = rtg::shade_pixel<S, 2>(sc, cam, x, y); break;
+      case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
+      default: p = rtg::shade_pixel<S, 2, true>(sc, cam, x, y); break;
     }
     out[3 * x + 0] = p.x;
     out[3 * x + 1] = p.y;

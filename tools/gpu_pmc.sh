@@ -10,8 +10,8 @@ mkdir -p $OUT/pmc_$TAG
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $OUT/pmc_$TAG/counters_list.txt 2>&1 || true
 i=0
-GROUPS=${GROUPS:-"FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"}
-IFS='|' read -ra GRPS <<< "$GROUPS"
+PMC_GROUPS=${PMC_GROUPS:-"FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"}
+IFS='|' read -ra GRPS <<< "$PMC_GROUPS"
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
   echo "== pass $i: $grp"
