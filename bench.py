@@ -115,6 +115,9 @@ def main():
                     "once after timing; reports s_memtime cycle shares per phase")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: gather through host memory (lets N ranks share one GPU "
+                         "to exercise the multi-rank path on a 1-GPU box)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,9 +125,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # only differs when ranks share a GPU (gloo rehearsal)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     W, H, n, m, depth = CONFIGS[args.config]
     S = depth + 1
@@ -156,7 +164,14 @@ def main():
         if i is not None:
             ev_k[i][1].record(stream)
         if world > 1:
-            dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if args.dist_backend == "nccl":  # ONE RCCL gather over xGMI
+                dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            else:                            # rehearsal path through host memory
+                host = shard.cpu()
+                gl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+                dist.gather(host, gl, dst=0)
+                if rank == 0:
+                    gathered.copy_(torch.stack(gl))
             if rank == 0:
                 frame = rdist.assemble(gathered, H, B).contiguous()
         else:
@@ -178,7 +193,8 @@ def main():
     elapsed = t1 - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_k]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_max_ms = float(t[0]), float(t[1])
     else:
@@ -298,7 +314,9 @@ def main():
                                f"(RTSTACK_MAXSIZE {S}), 3x3 supersampling",
                    "width": W, "height": H, "spheres": n, "lights": m, "depth": depth,
                    "alias_factor": 3, "row_block": B, "variant": args.variant,
-                   "parallelism": f"row-cyclic x{world}" + (" + RCCL gather" if world > 1 else "")},
+                   "parallelism": f"row-cyclic x{world}" + (
+                       (" + RCCL gather" if args.dist_backend == "nccl" else " + gloo gather")
+                       if world > 1 else "")},
         "mrays_per_s": round(mpx * 9, 1),
         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
         "roofline": roof, "cpu_baseline": cpu,

@@ -520,6 +520,11 @@ int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
     rtg_set_error("rtg_render_rows: null argument");
     return RTG_ERR_INVALID;
   }
+  if (nRows) {
+    int rc0 = check_render_args(spheres, sphNum, lights, lgtNum, width, height, zoom,
+                                aliasFactor, stackSize, dstHost);
+    if (rc0) return rc0;
+  }
   for (unsigned k = 0; k < nRows; ++k)
     if (rows[k] >= height) {
       rtg_set_error("rtg_render_rows: row %u >= height %u", rows[k], height);
@@ -594,14 +599,33 @@ int rtg_ppm_bytes_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n
   return RTG_OK;
 }
 
+// Argument checks shared by the one-shot entry points (no HIP call made).
+static int check_render_args(const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
+                             unsigned lgtNum, unsigned width, unsigned height, float zoom,
+                             float aliasFactor, int stackSize, const void* dst) {
+  if (!dst) {
+    rtg_set_error("render: null destination");
+    return RTG_ERR_INVALID;
+  }
+  if ((sphNum && !spheres) || (lgtNum && !lights)) {
+    rtg_set_error("render: null scene array");
+    return RTG_ERR_INVALID;
+  }
+  if (stackSize < 1 || stackSize > RTG_MAX_STACK) {
+    rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
+    return RTG_ERR_INVALID;
+  }
+  Camera cam;
+  return make_camera(width, height, zoom, aliasFactor, &cam);
+}
+
 int rtg_render(int device, const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
                unsigned lgtNum, unsigned width, unsigned height, float zoom, float aliasFactor,
                int stackSize, rtg_vec* dstHost) {
   rtg_clear_error();
-  if (!dstHost) {
-    rtg_set_error("rtg_render: null destination");
-    return RTG_ERR_INVALID;
-  }
+  int rc0 = check_render_args(spheres, sphNum, lights, lgtNum, width, height, zoom, aliasFactor,
+                              stackSize, dstHost);
+  if (rc0) return rc0;
   rtg_context* ctx = nullptr;
   int rc = rtg_context_create(device, &ctx);
   if (rc) return rc;
