@@ -313,6 +313,26 @@ static void free_scene(rtg_context* c) {
   c->hasScene = false;
 }
 
+// Argument checks shared by the one-shot entry points (no HIP call made).
+static int check_render_args(const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
+                             unsigned lgtNum, unsigned width, unsigned height, float zoom,
+                             float aliasFactor, int stackSize, const void* dst) {
+  if (!dst) {
+    rtg_set_error("render: null destination");
+    return RTG_ERR_INVALID;
+  }
+  if ((sphNum && !spheres) || (lgtNum && !lights)) {
+    rtg_set_error("render: null scene array");
+    return RTG_ERR_INVALID;
+  }
+  if (stackSize < 1 || stackSize > RTG_MAX_STACK) {
+    rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
+    return RTG_ERR_INVALID;
+  }
+  Camera cam;
+  return make_camera(width, height, zoom, aliasFactor, &cam);
+}
+
 extern "C" {
 
 int rtg_device_count(int* count) {
@@ -597,26 +617,6 @@ int rtg_ppm_bytes_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n
                      (const float*)pixelsDevice, nval, maxDevice, outDevice);
   HIP_TRY(hipGetLastError());
   return RTG_OK;
-}
-
-// Argument checks shared by the one-shot entry points (no HIP call made).
-static int check_render_args(const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
-                             unsigned lgtNum, unsigned width, unsigned height, float zoom,
-                             float aliasFactor, int stackSize, const void* dst) {
-  if (!dst) {
-    rtg_set_error("render: null destination");
-    return RTG_ERR_INVALID;
-  }
-  if ((sphNum && !spheres) || (lgtNum && !lights)) {
-    rtg_set_error("render: null scene array");
-    return RTG_ERR_INVALID;
-  }
-  if (stackSize < 1 || stackSize > RTG_MAX_STACK) {
-    rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
-    return RTG_ERR_INVALID;
-  }
-  Camera cam;
-  return make_camera(width, height, zoom, aliasFactor, &cam);
 }
 
 int rtg_render(int device, const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
