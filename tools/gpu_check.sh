@@ -16,6 +16,10 @@ cat $OUT/smoke_$TAG.log &&
 echo "== bench" &&
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 3 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err &&
 cat $OUT/bench_$TAG.json &&
+echo "== 2-rank rehearsal (gloo gather, both ranks on this GPU)" &&
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+    bench.py --gpus 2 --steps 5 --warmup 1 --dist-backend gloo > $OUT/bench2_$TAG.json 2> $OUT/bench2_$TAG.err &&
+python -c "import json;l=[x for x in open('$OUT/bench2_$TAG.json') if x.startswith('{')][-1];print('2-rank parity', json.loads(l)['parity'])" &&
 echo "== rocprofv3 kernel trace" &&
 ( cd /tmp && export TMPDIR=/tmp &&
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/prof_$TAG" -o run \
