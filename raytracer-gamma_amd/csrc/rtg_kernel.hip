@@ -183,13 +183,42 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned x = blockIdx.x * kTileW + (wave & 1u) * 8u + (lane & 7u);
   const unsigned lr = blockIdx.y * kTileH + (wave >> 1) * 8u + (lane >> 3);
-  if (x >= a.W || lr >= a.rowsLocal) return;
-  const unsigned gy =
-      a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
+  const bool valid = x < a.W && lr < a.rowsLocal;
+  const unsigned gy = !valid ? 0u
+                     : a.rowList ? a.rowList[lr]
+                                 : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
+
+  // Primary-ray sphere cull for this wave (whole wave converged here): the
+  // bounds of every sample direction of the wave's pixels, then one sphere
+  // per lane against that bundle, then a ballot (see primary_sphere_possible).
+  uint64_t primSel = ~0ull;
+  bool usePrim = false;
+  if constexpr (kBase == 0) {
+    if (a.n <= 64) {
+      float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
+      if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
+      for (int off = 32; off > 0; off >>= 1) {
+        x0 = fminf(x0, __shfl_xor(x0, off));
+        x1 = fmaxf(x1, __shfl_xor(x1, off));
+        y0 = fminf(y0, __shfl_xor(y0, off));
+        y1 = fmaxf(y1, __shfl_xor(y1, off));
+      }
+      bool possible = false;
+      if (lane < a.n) {
+        const float4 g = sc.lgeom[lane];
+        possible = primary_sphere_possible(v3(g.x, g.y, g.z), sqrtf(g.w), x0, x1, y0, y1,
+                                           a.cam.zoom);
+      }
+      primSel = __ballot(possible);
+      usePrim = true;
+    }
+  }
+  if (!valid) return;
   V3 pix;
   unsigned long long tk0 = 0;
   if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
-  if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
+  if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
+  else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
   else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
   else if constexpr (kBase == 2) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
@@ -254,6 +283,7 @@ typedef void (*TraceFn)(const KernelArgs);
 //   3 one-query-per-iteration state machine, four spheres per step
 //   4 node-persistent: samples chained in one node loop + candidate masks
 //   5 as 0 but frame colours in private memory instead of LDS
+//   6 as 0 without the per-wave primary-ray sphere cull
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
@@ -267,6 +297,7 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 1: return trace_fn_v<S, 1>(lds);
     case 4: return trace_fn_v<S, 4>(lds);
     case 5: return trace_fn_v<S, 5>(lds);
+    case 6: return trace_fn_v<S, 6>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
     default: return trace_fn_v<S, 0>(lds);

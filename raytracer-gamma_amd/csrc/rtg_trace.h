@@ -314,7 +314,8 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
 template <int S, int Q, class Scene, class FStore>
-RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc) {
+RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = false,
+                       uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   FrameR fr[NF];                        // reflection child rays (private memory)
   int sp = 0;                           // == level of the node being processed
@@ -325,7 +326,13 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc) {
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
     sc.probe_begin(kProbeClosest);
-    const int hit = query_closest<Q>(sc, o, d, t);
+    int hit;
+    if (usePrim) {  // the primary ray: only spheres its wave's bundle can reach
+      hit = closest_hit_sel(sc, o, d, t, primSel);
+      usePrim = false;
+    } else {
+      hit = query_closest<Q>(sc, o, d, t);
+    }
     sc.probe_end(kProbeClosest);
     sc.probe_begin(kProbeShade);
     if (hit < 0) {
@@ -573,6 +580,72 @@ RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
     }
   }
   return false;
+}
+
+// Closest hit restricted to a wave-uniform subset `sel` of spheres 0..63
+// (bit i = sphere i may be hit; see primary_sphere_mask).  Spheres outside
+// `sel` cannot produce a valid root, so the result equals closest_hit_mask's.
+template <class Scene>
+RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t sel) {
+  const RayQ q = make_query(o, d);
+  float minT = 1000.f;
+  int best = -1;
+  uint64_t cand = 0;
+  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform: scalar loop + scalar loads
+    const unsigned i = (unsigned)__builtin_ctzll(m);
+    float r2;
+    const V3 c = sc.sphere(i, r2);
+    const V3 disp = vsub(o, c);
+    const float b = 2.0f * vdot(d, disp);
+    const float cc = vdot(disp, disp) - r2;
+    const float rad = (b * b) - (q.a4 * cc);
+    cand |= (rad >= 0.0f) ? (1ull << i) : 0ull;
+  }
+  while (cand) {
+    const unsigned i = (unsigned)__builtin_ctzll(cand);
+    cand &= cand - 1;
+    float r2;
+    const V3 c = sc.sphere_lane(i, r2);
+    bool res;
+    const float t = ray_sphere(q, c, r2, res);
+    if (res && t < minT) { minT = t; best = (int)i; }
+  }
+  tOut = minT;
+  return best;
+}
+
+// Conservative cull of spheres for a bundle of primary rays (origin 0,
+// main.cpp:417): every ray direction is (X, Y, zoom) with X in [x0, x1],
+// Y in [y0, y1] (main.cpp:432-436, before normalisation).  Returns bit i set
+// unless sphere i provably has no forward intersection with any such ray:
+// its angular distance from the bundle's axis exceeds the bundle's half-angle
+// plus the sphere's angular radius by a 1e-3 rad margin (radius also inflated
+// by 1e-3 relative + 1e-3 absolute), far above the float error of either the
+// bounds or the reference's own root test.  Only spheres 0..63 can be culled
+// (bits are kept for all when n > 64 is handled by the caller).
+RTG_HD bool primary_sphere_possible(V3 c, float r, float x0, float x1, float y0, float y1,
+                                    float zoom) {
+  if (!(zoom != 0.f)) return true;
+  const float xc = 0.5f * (x0 + x1), yc = 0.5f * (y0 + y1);
+  const float la = sqrtf(xc * xc + yc * yc + zoom * zoom);
+  const V3 U = v3(xc / la, yc / la, zoom / la);
+  float cosTheta = 1.f;
+  const float xs[2] = {x0, x1}, ys[2] = {y0, y1};
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      const float lc = sqrtf(xs[a] * xs[a] + ys[b] * ys[b] + zoom * zoom);
+      const float cs = (U.x * xs[a] + U.y * ys[b] + U.z * zoom) / lc;
+      cosTheta = fminf(cosTheta, cs);
+    }
+  const float theta = acosf(fmaxf(-1.f, fminf(1.f, cosTheta)));
+  const float L = sqrtf(vdot(c, c));
+  const float rr = r * 1.001f + 1.0e-3f;
+  if (!(L > rr * 1.001f)) return true;  // origin inside or near the sphere (or NaN)
+  const float alpha = asinf(fminf(1.f, rr / L));
+  const float lim = theta + alpha + 1.0e-3f;
+  if (!(lim < 3.1f)) return true;
+  const float cosPhi = vdot(U, c) / L;
+  return cosPhi >= cosf(lim);
 }
 
 // Query strategy selector: 0 = one sphere per step with a branch per sphere,
@@ -896,9 +969,24 @@ RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsi
   return pix;
 }
 
+// Bounds of the primary-ray directions of pixel (x, y) (all its samples):
+// X = (pxX + j*st)*asp, Y = pxY + i*st for i, j in [0, nAA).
+RTG_HD void primary_bounds(const Camera& cam, unsigned x, unsigned y, float& x0, float& x1,
+                           float& y0, float& y1) {
+  const float pxX = (((float)x - cam.halfW)) * cam.xs;
+  const float pxY = (cam.halfH - (float)y) * cam.ys;
+  const float ext = (float)(cam.nAA > 0 ? cam.nAA - 1 : 0) * cam.st;
+  const float a = pxX * cam.asp, b = (pxX + ext) * cam.asp;
+  x0 = fminf(a, b);
+  x1 = fmaxf(a, b);
+  y0 = fminf(pxY, pxY + ext);
+  y1 = fmaxf(pxY, pxY + ext);
+}
+
 // main.cpp:411-452 for pixel (x, y) of the frame.
 template <int S, int Q, bool kSceneFrames = false, class Scene>
-RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y) {
+RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y,
+                      bool usePrim = false, uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   LocalFrames<NF> local;
   const float pxX = (((float)x - cam.halfW)) * cam.xs;
@@ -910,8 +998,8 @@ RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y
       const float ry = (pxY + (float)(((float)i) * cam.st));
       const V3 dir = vnorm(v3(rx, ry, cam.zoom));
       V3 c;
-      if constexpr (kSceneFrames) c = trace_sample<S, Q>(sc, dir, sc.frames());
-      else c = trace_sample<S, Q>(sc, dir, local);
+      if constexpr (kSceneFrames) c = trace_sample<S, Q>(sc, dir, sc.frames(), usePrim, primSel);
+      else c = trace_sample<S, Q>(sc, dir, local, usePrim, primSel);
       c = vsmul(cam.inv, c);
       pix = vadd(pix, c);
     }

@@ -68,7 +68,25 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 3: p = rtg::shade_pixel_persistent<S, 1>(sc, cam, x, y); break;
       case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
       case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
-      default: p = rtg::shade_pixel<S, 2, true>(sc, cam, x, y); break;
+      default: {
+        // per-pixel primary cull: a stricter (smaller) bundle than the GPU's
+        // per-wave one, so it exercises the cull's conservativeness harder
+        uint64_t sel = ~0ull;
+        bool use = sc.n <= 64;
+        if (use) {
+          float x0, x1, y0, y1;
+          rtg::primary_bounds(cam, x, y, x0, x1, y0, y1);
+          sel = 0;
+          for (unsigned k = 0; k < sc.n; ++k) {
+            float r2;
+            const rtg::V3 c = sc.sphere(k, r2);
+            if (rtg::primary_sphere_possible(c, sqrtf(r2), x0, x1, y0, y1, cam.zoom))
+              sel |= 1ull << k;
+          }
+        }
+        p = rtg::shade_pixel<S, 2, true>(sc, cam, x, y, use, sel);
+        break;
+      }
     }
     out[3 * x + 0] = p.x;
     out[3 * x + 1] = p.y;

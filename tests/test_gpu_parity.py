@@ -97,8 +97,10 @@ def test_random_scenes_vs_oracle(R, oracle):
         n, m = int(rng.integers(0, 20)), int(rng.integers(0, 5))
         W, H = int(rng.integers(1, 70)), int(rng.integers(1, 50))
         aa = float(rng.choice([1.0, 2.0, 3.0, 2.5, 4.0]))
-        zoom = float(rng.choice([-4.0, -2.0, -7.0]))
+        zoom = float(rng.choice([-4.0, -2.0, -7.0, 3.0, 0.5]))
         sph, lg = random_scene(rng, n, m)
+        if zoom > 0:
+            sph["pos"][:, 2] *= -1.0
         want = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
         got = R.render(sph, lg, W, H, zoom=zoom, alias_factor=aa, stack_size=S)
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
@@ -177,7 +179,7 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 100])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 100])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda

@@ -175,8 +175,10 @@ def test_kernel_traversal_random_scenes(hostsim, variant, oracle, rtg):
         n, m = int(rng.integers(0, 14)), int(rng.integers(0, 5))
         W, H = int(rng.integers(1, 40)), int(rng.integers(1, 30))
         aa = float(rng.choice([1.0, 2.0, 3.0, 2.5]))
-        zoom = float(rng.choice([-4.0, -2.0, -7.0]))
+        zoom = float(rng.choice([-4.0, -2.0, -7.0, 3.0, 0.5]))
         sph, lg = random_scene(rng, n, m)
+        if zoom > 0:  # put some spheres behind the camera plane's other side
+            sph["pos"][:, 2] *= -1.0
         want = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
         got = _hostsim_render(hostsim, sph, lg, W, H, S, aa=aa, zoom=zoom)
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
