@@ -62,9 +62,45 @@ struct LdsFrames {
   __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kBlock]; }
 };
 
+// Wave-wide reductions with DPP (all 64 lanes must be active: the converged
+// loop of trace_sample_cv guarantees it at every call site).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), kCtrl, kRowMask, 0xF, false));
+}
+struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+template <class Op>
+__device__ __forceinline__ float wave_reduce(float v) {
+  Op op;
+  v = op(v, dpp_f<0xB1, 0xF>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_f<0x4E, 0xF>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_f<0x141, 0xF>(v));  // row_half_mirror
+  v = op(v, dpp_f<0x140, 0xF>(v));  // row_mirror: every lane holds its row's result
+  v = op(v, dpp_f<0x142, 0xA>(v));  // row_bcast:15 into rows 1, 3
+  v = op(v, dpp_f<0x143, 0xC>(v));  // row_bcast:31 into rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 template <class MatPtr, bool kDiag = false>
 struct DevScene {
   FrameC* lfr;
+  __device__ __forceinline__ bool any(bool b) const { return __ballot(b) != 0ull; }
+  __device__ __forceinline__ float wave_max(float v) const { return wave_reduce<OpMax>(v); }
+  __device__ __forceinline__ int first_lane(bool b) const {
+    const uint64_t m = __ballot(b);
+    return m ? (int)__builtin_ctzll(m) : -1;
+  }
+  __device__ __forceinline__ float read_lane(float v, int l) const {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+  }
+  // bit k (k < min(n, 64)) = pred(k), evaluated by lane k.
+  template <class F>
+  __device__ __forceinline__ uint64_t sphere_mask(F pred) const {
+    const unsigned lane = threadIdx.x & 63u;
+    const bool p = (lane < n) ? pred(lane) : false;
+    return __ballot(p);
+  }
   __device__ __forceinline__ LdsFrames frames() const { return LdsFrames{lfr}; }
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
@@ -193,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   // per lane against that bundle, then a ballot (see primary_sphere_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if constexpr (kBase == 0) {
+  if constexpr (kBase == 0 || kBase == 7) {
     if (a.n <= 64) {
       float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
       if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
@@ -213,17 +249,21 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
       usePrim = true;
     }
   }
-  if (!valid) return;
+  if constexpr (kBase != 7) {
+    if (!valid) return;
+  }
   V3 pix;
   unsigned long long tk0 = 0;
   if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
   if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 7) pix = shade_pixel_cv<S>(sc, a.cam, x, gy, valid, usePrim, primSel);
   else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
   else if constexpr (kBase == 2) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
   else if constexpr (kBase == 3) pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
   else pix = shade_pixel_nodes<S, 2>(sc, a.cam, x, gy);
+  if (!valid) return;  // (variant 7 keeps every lane until here)
   if constexpr (kDiag) {
     sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
     // one wave-level add per slot (values are wave-uniform: s_memtime is scalar)
@@ -284,6 +324,7 @@ typedef void (*TraceFn)(const KernelArgs);
 //   4 node-persistent: samples chained in one node loop + candidate masks
 //   5 as 0 but frame colours in private memory instead of LDS
 //   6 as 0 without the per-wave primary-ray sphere cull
+//   7 converged per-sample loop with per-query bundle culling (trace_sample_cv)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
@@ -298,6 +339,8 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 4: return trace_fn_v<S, 4>(lds);
     case 5: return trace_fn_v<S, 5>(lds);
     case 6: return trace_fn_v<S, 6>(lds);
+    case 7: return trace_fn_v<S, 7>(lds);
+    case 107: return trace_fn_v<S, 107>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
     default: return trace_fn_v<S, 0>(lds);

@@ -33,6 +33,17 @@ struct HostScene {
     rtg::FrameC& operator()(int lv) const { return f[lv]; }
   };
   mutable rtg::FrameC fr[16];
+  bool any(bool b) const { return b; }
+  float wave_max(float v) const { return v; }
+  int first_lane(bool b) const { return b ? 0 : -1; }
+  float read_lane(float v, int) const { return v; }
+  template <class F>
+  uint64_t sphere_mask(F pred) const {
+    uint64_t m = 0;
+    for (unsigned k = 0; k < n && k < 64; ++k)
+      if (pred(k)) m |= 1ull << k;
+    return m;
+  }
   Frames frames() const { return Frames{fr}; }
   void probe_end(int) const {}
   void sphere4(unsigned i, rtg::V3* c, float* r2) const {
@@ -68,6 +79,23 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 3: p = rtg::shade_pixel_persistent<S, 1>(sc, cam, x, y); break;
       case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
       case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
+      case 7: {
+        uint64_t sel = ~0ull;
+        bool use = sc.n <= 64;
+        if (use) {
+          float x0, x1, y0, y1;
+          rtg::primary_bounds(cam, x, y, x0, x1, y0, y1);
+          sel = 0;
+          for (unsigned k = 0; k < sc.n; ++k) {
+            float r2;
+            const rtg::V3 c = sc.sphere(k, r2);
+            if (rtg::primary_sphere_possible(c, sqrtf(r2), x0, x1, y0, y1, cam.zoom))
+              sel |= 1ull << k;
+          }
+        }
+        p = rtg::shade_pixel_cv<S>(sc, cam, x, y, true, use, sel);
+        break;
+      }
       default: {
         // per-pixel primary cull: a stricter (smaller) bundle than the GPU's
         // per-wave one, so it exercises the cull's conservativeness harder
