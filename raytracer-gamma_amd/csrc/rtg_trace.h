@@ -986,34 +986,42 @@ RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsi
 // Scene interface used: any(bool), wave_min/max/sum(float) over the wave (the
 // host simulation is a wave of one lane), sphere_mask(pred) -> bit k = pred(k).
 
-// Subset of spheres that any ray of the bundle can reach with t > 0.
-RTG_HD bool bundle_sphere_possible(V3 c, float r, V3 O, float rho, V3 U, float theta) {
+// Subset of spheres that any ray of the bundle can reach with t > 0.  The
+// bundle is all rays from ball(O, rho) with unit directions within angle
+// theta of U (cosT, sinT given).  Keep iff angle(U, c - O) <= theta + alpha,
+// alpha = asin(rr / |c - O|): compared through cos(theta + alpha) =
+// cosT cos(alpha) - sinT sin(alpha), minus a 2e-3 margin (cos is
+// 1-Lipschitz, so that covers an angle margin of 2e-3 rad).
+RTG_HD bool bundle_sphere_possible(V3 c, float r, V3 O, float rho, V3 U, float cosT,
+                                   float sinT) {
   const V3 v = vsub(c, O);
-  const float L = sqrtf(vdot(v, v));
+  const float L2 = vdot(v, v);
   const float rr = (r + rho) * 1.001f + 1.0e-3f;
-  if (!(L > rr * 1.001f)) return true;
-  const float alpha = asinf(fminf(1.f, rr / L));
-  const float lim = theta + alpha + 1.0e-3f;
-  if (!(lim < 3.1f)) return true;
-  return vdot(U, v) / L >= cosf(lim);
+  if (!(L2 > rr * rr * 1.002f)) return true;
+  const float L = sqrtf(L2);
+  const float sa = rr / L;
+  const float ca = sqrtf(fmaxf(0.f, 1.f - sa * sa));
+  const float cl = cosT * ca - sinT * sa;  // cos(theta + alpha)
+  if (!(cl > -0.98f)) return true;          // theta + alpha near pi: keep
+  return vdot(U, v) >= (cl - 2.0e-3f) * L;
 }
 
-// Can sphere (c, r) meet a segment from a point of ball(O, rho) to the light Lp?
-RTG_HD bool shadow_sphere_possible(V3 c, float r, V3 O, float rho, V3 Lp) {
-  const V3 A = vsub(O, Lp);
-  const float DA = sqrtf(vdot(A, A));
-  const float rb = rho * 1.001f + 1.0e-3f;
-  if (!(DA > rb * 1.001f)) return true;
+// Can sphere (c, r) meet a segment from a point of ball(O, rho) to the light
+// point Lp?  The segments lie in the cone with apex Lp, axis A = O - Lp and
+// half-angle beta = asin(rb / |A|) (sb, cb given), within distance |A| + rb of Lp.
+RTG_HD bool shadow_sphere_possible(V3 c, float r, V3 A, float DA, float rb, float sb, float cb,
+                                   V3 Lp) {
   const V3 v = vsub(c, Lp);
-  const float L = sqrtf(vdot(v, v));
+  const float L2 = vdot(v, v);
   const float rr = r * 1.001f + 1.0e-3f;
-  if (!(L > rr * 1.001f)) return true;
+  if (!(L2 > rr * rr * 1.002f)) return true;
+  const float L = sqrtf(L2);
   if (L - rr > (DA + rb) * 1.001f + 1.0e-3f) return false;  // beyond every segment's end
-  const float beta = asinf(fminf(1.f, rb / DA));
-  const float alpha = asinf(fminf(1.f, rr / L));
-  const float lim = beta + alpha + 1.0e-3f;
-  if (!(lim < 3.1f)) return true;
-  return vdot(A, v) / (DA * L) >= cosf(lim);
+  const float sa = rr / L;
+  const float ca = sqrtf(fmaxf(0.f, 1.f - sa * sa));
+  const float cl = cb * ca - sb * sa;
+  if (!(cl > -0.98f)) return true;
+  return vdot(A, v) >= (cl - 2.0e-3f) * (DA * L);
 }
 
 // Ball bounding the points p of participating lanes (converged call): centred
@@ -1047,13 +1055,13 @@ RTG_HD uint64_t closest_bundle_sel(const Scene& sc, bool part, V3 o, V3 d) {
   const V3 u = ok ? vsmul(1.f / sqrtf(dd), d) : v3(0.f, 0.f, 0.f);
   const int l0 = sc.first_lane(ok);
   const V3 U = v3(sc.read_lane(u.x, l0), sc.read_lane(u.y, l0), sc.read_lane(u.z, l0));
-  const float cmin = -sc.wave_max(ok ? -vdot(u, U) : -2.f);
-  const float theta = acosf(fmaxf(-1.f, fminf(1.f, cmin))) * 1.001f + 1.0e-3f;
-  if (!(theta < 1.5f)) return ~0ull;
+  const float cosT = fminf(1.f, -sc.wave_max(ok ? -vdot(u, U) : -2.f)) - 1.0e-4f;
+  if (!(cosT > 0.1f)) return ~0ull;  // bundle too wide to be worth a test
+  const float sinT = sqrtf(fmaxf(0.f, 1.f - cosT * cosT));
   return sc.sphere_mask([&](unsigned k) {
     float r2;
     const V3 c = sc.sphere_lane(k, r2);
-    return bundle_sphere_possible(c, sqrtf(r2), O, rho, U, theta);
+    return bundle_sphere_possible(c, sqrtf(r2), O, rho, U, cosT, sinT);
   });
 }
 
@@ -1148,12 +1156,20 @@ RTG_HD V3 trace_sample_cv(const Scene& sc, V3 dir0, FStore&& fc, bool active, bo
         }
         if (!sc.any(need)) continue;
         uint64_t selL = ~0ull;
-        if (cullS)
-          selL = sc.sphere_mask([&](unsigned k) {
-            float r2;
-            const V3 c = sc.sphere_lane(k, r2);
-            return shadow_sphere_possible(c, sqrtf(r2), O, rho, Lpos);
-          });
+        if (cullS) {
+          const V3 A = vsub(O, Lpos);
+          const float DA = sqrtf(vdot(A, A));
+          const float rb = rho * 1.001f + 1.0e-3f;
+          if (DA > rb * 1.01f) {
+            const float sb = rb / DA;
+            const float cb = sqrtf(fmaxf(0.f, 1.f - sb * sb));
+            selL = sc.sphere_mask([&](unsigned k) {
+              float r2;
+              const V3 c = sc.sphere_lane(k, r2);
+              return shadow_sphere_possible(c, sqrtf(r2), A, DA, rb, sb, cb, Lpos);
+            });
+          }
+        }
         sc.probe_begin(kProbeShadow);
         if (need) {
           const bool blk = cull ? blocked_sel(sc, P, dir, gap, selL)
