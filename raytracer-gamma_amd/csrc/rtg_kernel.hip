@@ -77,9 +77,11 @@ __device__ __forceinline__ float wave_reduce(float v) {
   v = op(v, dpp_f<0x4E, 0xF>(v));   // quad_perm [2,3,0,1]
   v = op(v, dpp_f<0x141, 0xF>(v));  // row_half_mirror
   v = op(v, dpp_f<0x140, 0xF>(v));  // row_mirror: every lane holds its row's result
-  v = op(v, dpp_f<0x142, 0xA>(v));  // row_bcast:15 into rows 1, 3
-  v = op(v, dpp_f<0x143, 0xC>(v));  // row_bcast:31 into rows 2, 3
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 15));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 31));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 47));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+  return op(op(r0, r1), op(r2, r3));
 }
 
 template <class MatPtr, bool kDiag = false>
