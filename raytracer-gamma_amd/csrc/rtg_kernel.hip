@@ -97,6 +97,7 @@ struct DevScene {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
   }
   // bit k (k < min(n, 64)) = pred(k), evaluated by lane k.
+  __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
   template <class F>
   __device__ __forceinline__ uint64_t sphere_mask(F pred) const {
     const unsigned lane = threadIdx.x & 63u;
@@ -128,6 +129,7 @@ struct DevScene {
   const float4* lgeom;  // LDS copy of geom (or the global array when it does not fit)
   cfloat_p lights;
   unsigned n, m;
+  unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
   __device__ __forceinline__ V3 sphere(unsigned i, float& r2) const {
     cfloat_p g = geom + 4 * i;
@@ -172,7 +174,7 @@ struct KernelArgs {
   const float* crad2;
   const float* mats;
   const float* lights;
-  unsigned n, m;
+  unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
   const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
     const unsigned nm = (a.n + 1) * 8;
     for (unsigned i = threadIdx.x; i < nm; i += kBlock) lmats[i] = a.mats[i];
     float4* lg = sceneLds + (a.n + 1) * 2;
-    for (unsigned i = threadIdx.x; i < a.n; i += kBlock)
+    for (unsigned i = threadIdx.x; i < a.n4; i += kBlock)
       lg[i] = reinterpret_cast<const float4*>(a.geom)[i];
     __syncthreads();
     sc.mats = lmats;
@@ -218,6 +220,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   sc.lights = (cfloat_p)a.lights;
   sc.n = a.n;
   sc.m = a.m;
+  sc.n4 = a.n4;
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned x = blockIdx.x * kTileW + (wave & 1u) * 8u + (lane & 7u);
   const unsigned lr = blockIdx.y * kTileH + (wave >> 1) * 8u + (lane >> 3);
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   // per lane against that bundle, then a ballot (see primary_sphere_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if constexpr (kBase == 0 || kBase == 7) {
+  if constexpr (kBase == 0 || kBase == 7 || kBase == 8) {
     if (a.n <= 64) {
       float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
       if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
@@ -259,6 +262,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
   if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
+  else if constexpr (kBase == 8) pix = shade_pixel<S, 3, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 7) pix = shade_pixel_cv<S>(sc, a.cam, x, gy, valid, usePrim, primSel);
   else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
@@ -327,6 +331,7 @@ typedef void (*TraceFn)(const KernelArgs);
 //   5 as 0 but frame colours in private memory instead of LDS
 //   6 as 0 without the per-wave primary-ray sphere cull
 //   7 converged per-sample loop with per-query bundle culling (trace_sample_cv)
+//   8 as 0 with the tuned two-pass query (prefetched groups, uniform quotient path)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
@@ -342,6 +347,8 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 5: return trace_fn_v<S, 5>(lds);
     case 6: return trace_fn_v<S, 6>(lds);
     case 7: return trace_fn_v<S, 7>(lds);
+    case 8: return trace_fn_v<S, 8>(lds);
+    case 108: return trace_fn_v<S, 108>(lds);
     case 107: return trace_fn_v<S, 107>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
@@ -364,7 +371,7 @@ static TraceFn pick_trace(int S, bool lds, int variant) {
 
 struct rtg_context {
   int device = 0;
-  unsigned n = 0, m = 0;
+  unsigned n = 0, m = 0, n4 = 0;
   float4* geom = nullptr;
   float* crad2 = nullptr;
   float* mats = nullptr;
@@ -518,6 +525,7 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   HIP_TRY(hipMemcpy(ctx->lights, lg.data(), lg.size() * sizeof(float), hipMemcpyHostToDevice));
   ctx->n = sphNum;
   ctx->m = lgtNum;
+  ctx->n4 = ps.n4;
   ctx->hasScene = true;
   return RTG_OK;
 }
@@ -560,6 +568,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.lights = ctx->lights;
   a.n = ctx->n;
   a.m = ctx->m;
+  a.n4 = ctx->n4;
   a.W = width;
   a.rowsLocal = rows;
   a.rowBlock = rowBlock ? rowBlock : 1;
@@ -579,7 +588,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   dim3 grid((width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
   const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * kBlock * 16;
   const size_t lds = frameLds + (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) +
-                                            (size_t)ctx->n * 16)
+                                            (size_t)ctx->n4 * 16)
                                          : 0);
   hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());

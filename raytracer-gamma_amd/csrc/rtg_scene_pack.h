@@ -19,20 +19,24 @@
 
 namespace rtg {
 
-// Device image of a scene.  geom: n x {x, y, z, r*r}; crad2: n x (r+1e-6)^2;
+// Device image of a scene.  geom: n x {x, y, z, r*r} followed by NaN padding
+// records up to n4 + 4 (n4 = n rounded up to 4); crad2: n x (r+1e-6)^2;
 // mats: (n+1) x {matte.xyz, gloss.xyz, opacity, n} with [n] = background
 // {0,0,0, 0,0,0, 0, 1.0} (raytracer.h:694-697; opacity 0);
 // lights: m x {pos.xyz, col.xyz}.  Arrays are never empty (padded to 1).
 struct PackedScene {
   std::vector<float> geom, crad2, mats, lights;
   unsigned n = 0, m = 0;
+  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds n4 + 4 records
 };
 
 inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                        unsigned m, PackedScene* ps) {
   ps->n = n;
   ps->m = m;
-  ps->geom.assign((size_t)(n ? n : 1) * 4, 0.f);
+  ps->n4 = (n + 3u) & ~3u;
+  // Padding records are NaN spheres: their radicand is NaN, never >= 0.
+  ps->geom.assign((size_t)(ps->n4 + 4) * 4, __builtin_nanf(""));
   ps->crad2.assign(n ? n : 1, 0.f);
   ps->mats.assign((size_t)(n + 1) * 8, 0.f);
   ps->lights.assign((size_t)(m ? m : 1) * 6, 0.f);

@@ -648,17 +648,150 @@ RTG_HD bool primary_sphere_possible(V3 c, float r, float x0, float x1, float y0,
   return cosPhi >= cosf(lim);
 }
 
+// Two-pass query for scenes of at most 64 spheres (the common case), tuned:
+//  * the geometry array is padded with NaN spheres to a multiple of 4 plus one
+//    extra group (PackedScene), so pass 1 has no remainder loop and can load
+//    the next group of 4 records (one 64-byte scalar load) while testing the
+//    current one; a NaN sphere's radicand is NaN, never a candidate;
+//  * candidate bits of spheres 0..31 and 32..63 go to two 32-bit masks
+//    (the half is wave-uniform);
+//  * the Markstein quotient path is chosen once per query for the whole wave
+//    when every lane's denominator is in range (all(q.fast)), so pass 2 has no
+//    per-quotient branch.
+template <class Scene>
+RTG_HD void candidate_masks64(const Scene& sc, V3 o, V3 d, float a4, unsigned& lo,
+                              unsigned& hi) {
+  lo = 0;
+  hi = 0;
+  const unsigned n4 = sc.n4;
+  V3 c[4];
+  float r2[4];
+  sc.sphere4(0, c, r2);
+  for (unsigned k = 0; k < n4; k += 4) {
+    V3 cn[4];
+    float rn[4];
+    sc.sphere4(k + 4, cn, rn);  // in bounds: one padding group past n4
+    unsigned bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const V3 disp = vsub(o, c[q]);
+      const float b = 2.0f * vdot(d, disp);
+      const float cc = vdot(disp, disp) - r2[q];
+      const float rad = (b * b) - (a4 * cc);
+      bits |= (rad >= 0.0f) ? (1u << q) : 0u;
+    }
+    if (k < 32) lo |= bits << k;
+    else hi |= bits << (k - 32);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { c[q] = cn[q]; r2[q] = rn[q]; }
+  }
+}
+
+template <bool kFast>
+RTG_HD float quot_k(float x, const RayQ& q) {
+  if constexpr (kFast) {
+    const float q0 = x * q.y;
+    const float r0 = fmaf(-q0, q.den, x);
+    const float q1 = fmaf(r0, q.y, q0);
+    const float r1 = fmaf(-q1, q.den, x);
+    return fmaf(r1, q.y, q1);
+  } else {
+    return quot(x, q);
+  }
+}
+
+template <bool kFast>
+RTG_HD float ray_sphere_k(const RayQ& q, V3 c, float r2, bool& res) {
+  V3 disp = vsub(q.o, c);
+  const float b = 2.0f * vdot(q.d, disp);
+  const float cc = vdot(disp, disp) - r2;
+  const float radicand = (b * b) - (q.a4 * cc);
+  float sm = 10000.f;
+  res = false;
+  if (radicand >= 0.0f) {
+    const float root = rtg_sqrtf(radicand);
+    const float u0 = quot_k<kFast>(-b + root, q);
+    const float u1 = quot_k<kFast>(-b - root, q);
+    if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+    if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
+  }
+  return sm;
+}
+
+// Pass 2 over the candidates of one 32-sphere half; kShadow: stop at the first
+// blocker (gap given), else closest hit (minT/best updated).
+template <bool kFast, bool kShadow, class Scene>
+RTG_HD bool pass2(const Scene& sc, const RayQ& q, unsigned mask, unsigned base, float gap,
+                  float& minT, int& best) {
+  while (mask) {
+    const unsigned i = base + (unsigned)__builtin_ctz(mask);
+    mask &= mask - 1;
+    float r2;
+    const V3 c = sc.sphere_lane(i, r2);
+    bool res;
+    const float t = ray_sphere_k<kFast>(q, c, r2, res);
+    if constexpr (kShadow) {
+      if (res && t < 1000.f) {
+        const V3 dist = vsmul(t, q.d);
+        if (vdot(dist, dist) < gap) return true;
+      }
+    } else {
+      if (res && t < minT) { minT = t; best = (int)i; }
+    }
+  }
+  return false;
+}
+
+template <class Scene>
+RTG_HD int closest_hit64(const Scene& sc, V3 o, V3 d, float& tOut) {
+  const RayQ q = make_query(o, d);
+  unsigned lo, hi;
+  candidate_masks64(sc, o, d, q.a4, lo, hi);
+  float minT = 1000.f;
+  int best = -1;
+  if (sc.all(q.fast)) {
+    pass2<true, false>(sc, q, lo, 0, 0.f, minT, best);
+    pass2<true, false>(sc, q, hi, 32, 0.f, minT, best);
+  } else {
+    pass2<false, false>(sc, q, lo, 0, 0.f, minT, best);
+    pass2<false, false>(sc, q, hi, 32, 0.f, minT, best);
+  }
+  tOut = minT;
+  return best;
+}
+
+template <class Scene>
+RTG_HD bool blocked64(const Scene& sc, V3 o, V3 d, float gap) {
+  const RayQ q = make_query(o, d);
+  unsigned lo, hi;
+  candidate_masks64(sc, o, d, q.a4, lo, hi);
+  float minT = 0.f;
+  int best = 0;
+  if (sc.all(q.fast))
+    return pass2<true, true>(sc, q, lo, 0, gap, minT, best) ||
+           pass2<true, true>(sc, q, hi, 32, gap, minT, best);
+  return pass2<false, true>(sc, q, lo, 0, gap, minT, best) ||
+         pass2<false, true>(sc, q, hi, 32, gap, minT, best);
+}
+
 // Query strategy selector: 0 = one sphere per step with a branch per sphere,
-// 1 = four spheres per step, 2 = two-pass candidate masks.
+// 1 = four spheres per step, 2 = two-pass candidate masks, 3 = the tuned
+// two-pass query (<= 64 spheres; larger scenes fall back to 2).
 template <int Q, class Scene>
 RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t) {
   if constexpr (Q == 0) return closest_hit(sc, o, d, t);
   else if constexpr (Q == 1) return closest_hit4(sc, o, d, t);
-  else return closest_hit_mask(sc, o, d, t);
+  else if constexpr (Q == 3) {
+    if (sc.n4 <= 64) return closest_hit64(sc, o, d, t);
+    return closest_hit_mask(sc, o, d, t);
+  } else return closest_hit_mask(sc, o, d, t);
 }
 template <int Q, class Scene>
 RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap) {
-  if constexpr (Q == 2) return blocked_mask(sc, o, d, gap);
+  if constexpr (Q == 3) {
+    if (sc.n4 <= 64) return blocked64(sc, o, d, gap);
+    return blocked_mask(sc, o, d, gap);
+  } else if constexpr (Q == 2) return blocked_mask(sc, o, d, gap);
   else return blocked(sc, o, d, gap);
 }
 

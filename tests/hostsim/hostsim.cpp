@@ -20,7 +20,8 @@ struct HostScene {
   const float* crad2;
   const float* mats;
   const float* lights;
-  unsigned n, m;
+  unsigned n, m, n4;
+  bool all(bool b) const { return b; }
   rtg::V3 sphere(unsigned i, float& r2) const {
     const float* g = geom + 4 * i;
     r2 = g[3];
@@ -79,6 +80,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 3: p = rtg::shade_pixel_persistent<S, 1>(sc, cam, x, y); break;
       case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
       case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
+      case 8: p = rtg::shade_pixel<S, 3, true>(sc, cam, x, y); break;
       case 7: {
         uint64_t sel = ~0ull;
         bool use = sc.n <= 64;
@@ -133,7 +135,7 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   rtg::pack_scene(spheres, n, lights, m, &ps);
   rtg::Camera cam;
   if (rtg::make_camera(W, H, zoom, aa, &cam)) return -1;
-  HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, m};
+  HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, m, ps.n4};
   for (unsigned k = 0; k < nrows; ++k) {
     float* o = out + (size_t)k * W * 3;
     switch (S) {
