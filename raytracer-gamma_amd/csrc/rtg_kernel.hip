@@ -187,8 +187,12 @@ __device__ __forceinline__ float canon_nan(float v) {
   return (v != v) ? __uint_as_float(0xFFC00000u) : v;
 }
 
+// Minimum waves per SIMD requested from the register allocator (variant 9).
+template <int kVariant>
+struct MinWaves { static constexpr int value = (kVariant % 100 == 9) ? 7 : 1; };
+
 template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(kBlock, MinWaves<kVariant>::value) void trace_kernel(const KernelArgs a) {
   // LDS image: per-lane frame colours ((S-1) x kBlock x 16 B), then, when
   // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
   extern __shared__ float4 lds4[];
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   // per lane against that bundle, then a ballot (see primary_sphere_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if constexpr (kBase == 0 || kBase == 7 || kBase == 8) {
+  if constexpr (kBase == 0 || kBase == 7 || kBase == 8 || kBase == 9) {
     if (a.n <= 64) {
       float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
       if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
@@ -263,6 +267,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(const KernelArgs a) {
   if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
   else if constexpr (kBase == 8) pix = shade_pixel<S, 3, true>(sc, a.cam, x, gy, usePrim, primSel);
+  else if constexpr (kBase == 9) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 7) pix = shade_pixel_cv<S>(sc, a.cam, x, gy, valid, usePrim, primSel);
   else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
@@ -332,6 +337,7 @@ typedef void (*TraceFn)(const KernelArgs);
 //   6 as 0 without the per-wave primary-ray sphere cull
 //   7 converged per-sample loop with per-query bundle culling (trace_sample_cv)
 //   8 as 0 with the tuned two-pass query (prefetched groups, uniform quotient path)
+//   9 as 0 compiled for 7 waves/SIMD (__launch_bounds__ min waves 7: <= 72 VGPRs)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
@@ -348,6 +354,7 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 6: return trace_fn_v<S, 6>(lds);
     case 7: return trace_fn_v<S, 7>(lds);
     case 8: return trace_fn_v<S, 8>(lds);
+    case 9: return trace_fn_v<S, 9>(lds);
     case 108: return trace_fn_v<S, 108>(lds);
     case 107: return trace_fn_v<S, 107>(lds);
     case 2: return trace_fn_v<S, 2>(lds);

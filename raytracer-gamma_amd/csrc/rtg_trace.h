@@ -1243,7 +1243,9 @@ RTG_HD V3 trace_sample_cv(const Scene& sc, V3 dir0, FStore&& fc, bool active, bo
   while (sc.any(live)) {
     // ---- closest query (raytracer.h:455), bundle-culled (converged here)
     uint64_t sel = ~0ull;
+    sc.probe_begin(kProbePush);  // (slot reused: cull overhead in this variant)
     if (cull) sel = (first && usePrim) ? primSel : closest_bundle_sel(sc, live, o, d);
+    sc.probe_end(kProbePush);
     first = false;
     float t = 1000.f;
     int hit = -1;
@@ -1252,6 +1254,7 @@ RTG_HD V3 trace_sample_cv(const Scene& sc, V3 dir0, FStore&& fc, bool active, bo
     sc.probe_end(kProbeClosest);
 
     // ---- stage 0 shading (raytracer.h:454-550)
+    sc.probe_begin(kProbeShade);
     const bool shade = live && hit >= 0 && significant(I);
     if (live && hit < 0) ret = vmul(I, sc.mat(rm).matte);        // :544
     V3 P = v3(0.f, 0.f, 0.f), N = v3(0.f, 0.f, 0.f);
@@ -1272,7 +1275,9 @@ RTG_HD V3 trace_sample_cv(const Scene& sc, V3 dir0, FStore&& fc, bool active, bo
     if (sc.any(doMatte)) {
       V3 O = v3(0.f, 0.f, 0.f);
       float rho = 0.f;
+      sc.probe_begin(kProbePush);
       const bool cullS = cull && wave_ball(sc, doMatte, P, O, rho);
+      sc.probe_end(kProbePush);
       sc.probe_begin(kProbeMatte);
       for (unsigned l = 0; l < sc.m; ++l) {
         V3 Lpos, Lcol;
@@ -1365,6 +1370,7 @@ RTG_HD V3 trace_sample_cv(const Scene& sc, V3 dir0, FStore&& fc, bool active, bo
         ret = colour;
       }
     }
+    sc.probe_end(kProbeShade);
     // ---- unwind (stages 1 and 2)
     if (live && !descended) {
       sc.probe_begin(kProbeUnwind);

@@ -179,7 +179,7 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 100, 107, 108])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 100, 107, 108])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda
