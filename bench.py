@@ -115,6 +115,10 @@ def main():
                     "once after timing; reports s_memtime cycle shares per phase")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather-chunks", type=int, default=4,
+                    help="N > 1: split each rank's rows into K chunks; each chunk is rendered "
+                         "then gathered asynchronously, so RCCL overlaps the next chunk's "
+                         "rendering (1 = render all, then one gather)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: gather through host memory (lets N ranks share one GPU "
                          "to exercise the multi-rank path on a 1-GPU box)")
@@ -152,6 +156,12 @@ def main():
     sptr = stream.cuda_stream
     ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for _ in range(args.steps)]
+    # N > 1: chunks of the padded shard (same row ranges on every rank); the
+    # global rows of this rank's real rows, for rtg_render_rows_device.
+    K = max(1, min(args.gather_chunks, Rmax)) if world > 1 else 1
+    bounds = [(Rmax * c) // K for c in range(K + 1)]
+    grow = torch.tensor(R.shard_row_indices(H, B, rank, world).astype(np.int64),
+                        dtype=torch.int32, device="cuda") if world > 1 else None
 
     frame = None
 
@@ -159,23 +169,37 @@ def main():
         nonlocal frame
         if i is not None:
             ev_k[i][0].record(stream)
-        ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, shard=rank,
-                          n_shards=world, stream=sptr)
-        if i is not None:
-            ev_k[i][1].record(stream)
-        if world > 1:
-            if args.dist_backend == "nccl":  # ONE RCCL gather over xGMI
-                dist.gather(shard, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+        if world == 1:
+            ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, shard=0,
+                              n_shards=1, stream=sptr)
+            if i is not None:
+                ev_k[i][1].record(stream)
+            frame = shard
+            return
+        works = []
+        for c in range(K):
+            r0, r1 = bounds[c], bounds[c + 1]
+            nreal = max(0, min(r1, my_rows) - r0)
+            if nreal > 0:
+                ctx.render_rows_device(W, H, grow.data_ptr() + 4 * r0, nreal,
+                                       shard.data_ptr() + 12 * W * r0, stack_size=S, stream=sptr)
+            piece = shard[r0:r1]
+            if args.dist_backend == "nccl":  # RCCL gather over xGMI, overlapped
+                outs = [gathered[g, r0:r1] for g in range(world)] if rank == 0 else None
+                works.append(dist.gather(piece, outs, dst=0, async_op=True))
             else:                            # rehearsal path through host memory
-                host = shard.cpu()
+                host = piece.cpu()
                 gl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
                 dist.gather(host, gl, dst=0)
                 if rank == 0:
-                    gathered.copy_(torch.stack(gl))
-            if rank == 0:
-                frame = rdist.assemble(gathered, H, B).contiguous()
-        else:
-            frame = shard
+                    for g in range(world):
+                        gathered[g, r0:r1].copy_(gl[g])
+        if i is not None:
+            ev_k[i][1].record(stream)
+        for w in works:
+            w.wait()
+        if rank == 0:
+            frame = rdist.assemble(gathered, H, B).contiguous()
 
     for _ in range(args.warmup):
         step()
@@ -315,8 +339,8 @@ def main():
                    "width": W, "height": H, "spheres": n, "lights": m, "depth": depth,
                    "alias_factor": 3, "row_block": B, "variant": args.variant,
                    "parallelism": f"row-cyclic x{world}" + (
-                       (" + RCCL gather" if args.dist_backend == "nccl" else " + gloo gather")
-                       if world > 1 else "")},
+                       ((f" + RCCL gather ({K} pipelined chunks)") if args.dist_backend == "nccl"
+                        else " + gloo gather") if world > 1 else "")},
         "mrays_per_s": round(mpx * 9, 1),
         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
         "roofline": roof, "cpu_baseline": cpu,

@@ -187,12 +187,19 @@ __device__ __forceinline__ float canon_nan(float v) {
   return (v != v) ? __uint_as_float(0xFFC00000u) : v;
 }
 
-// Minimum waves per SIMD requested from the register allocator (variant 9).
-template <int kVariant>
-struct MinWaves { static constexpr int value = (kVariant % 100 == 9) ? 7 : 1; };
+// Minimum waves per SIMD requested from the register allocator: 7 (<= 72
+// VGPRs) where the LDS image of S-1 frame levels still admits 7 workgroups
+// per CU (S <= 6 with a small scene); measured +1-2 % over the unconstrained
+// 78-VGPR build at 6 waves/SIMD (C3).  Variant 9 forces it for any S.
+template <int S, int kVariant>
+struct MinWaves {
+  static constexpr int value =
+      ((kVariant % 100 == 0 && S <= 6) || kVariant % 100 == 9) ? 7 : 1;
+};
 
 template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(kBlock, MinWaves<kVariant>::value) void trace_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_kernel(
+    const KernelArgs a) {
   // LDS image: per-lane frame colours ((S-1) x kBlock x 16 B), then, when
   // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
   extern __shared__ float4 lds4[];

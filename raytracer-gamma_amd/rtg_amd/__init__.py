@@ -266,6 +266,16 @@ class Context:
                                        ctypes.c_void_p(stream) if stream else None),
                "rtg_render_device")
 
+    def render_rows_device(self, width, height, rows_ptr: int, n_rows: int, dst_ptr: int,
+                           zoom=-4.0, alias_factor=3.0, stack_size=6, stream: int = 0):
+        """Render the global rows listed at rows_ptr (device uint32[n_rows])."""
+        _check(lib().rtg_render_rows_device(self._h, width, height, float(zoom),
+                                            float(alias_factor), stack_size,
+                                            ctypes.c_void_p(rows_ptr), n_rows,
+                                            ctypes.c_void_p(dst_ptr),
+                                            ctypes.c_void_p(stream) if stream else None),
+               "rtg_render_rows_device")
+
     def max_colour_device(self, src_ptr: int, n_pixels: int, dst_ptr: int, stream: int = 0):
         _check(lib().rtg_max_colour_device(self._h, ctypes.c_void_p(src_ptr), n_pixels,
                                            ctypes.c_void_p(dst_ptr),
