@@ -325,9 +325,22 @@ def main():
                         "peak_GBs": HBM_PEAK_GBS,
                         "frac": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
                         "algorithmic_bytes": my_rows * W * 12}}
-        tr = os.environ.get("RTG_PMC_TRAFFIC_BYTES")  # filled from profiles/ when known
-        if tr:
-            roof["traffic"] = int(tr)
+        # HBM traffic per launch from the committed PMC passes (tools/gpu_pmc.sh ->
+        # profiles/pmc_<config>.json), used only when measured on these kernel
+        # sources, this variant and N = 1.
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pmc) and world == 1:
+            rec = json.load(open(pmc))
+            import importlib.util
+            spec = importlib.util.spec_from_file_location(
+                "pmc_summary", os.path.join(ROOT, "tools", "pmc_summary.py"))
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            if rec.get("source_md5") == mod.source_md5() and rec.get("variant") == args.variant \
+                    and "traffic_bytes" in rec:
+                roof["traffic"] = int(rec["traffic_bytes"])
+                roof["traffic_note"] = ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
+                                        f"({pmc}); mostly private-memory reflection rays")
 
     out = {
         "metric": METRIC, "value": round(mpx, 2), "unit": "Mpixels/s", "n_gpus": world,

@@ -136,6 +136,11 @@ int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts);
  * {closest-hit queries, shadow queries, refraction, whole pixel} into 8
  * counters; read (and optionally zero) them.  Zeros for normal variants. */
 int rtg_diag_read(rtg_context* ctx, unsigned long long* out8, int reset);
+/* Wave timeline of the last launch of the timeline variant (13): one record
+ * per wave {start, end (s_memrealtime, 100 MHz, low 32 bits), HW_ID, XCC_ID},
+ * in launch order.  Copies min(cap, waves) records; *count = waves recorded.
+ * Diagnostic only (occupancy analysis, tools/timeline.py). */
+int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* count);
 
 /* ---- output side ---- */
 /* algebra.h:68-91 on the host. */

@@ -39,7 +39,7 @@
 
 namespace rtg {
 
-constexpr int kTileW = 16, kTileH = 16, kBlock = 256;
+constexpr int kBlock = 256;
 // Materials staged in LDS when the table fits (n+1 records of 32 B).
 constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 
@@ -57,54 +57,19 @@ typedef const RTG_CONST float* cfloat_p;
 // Per-lane frame colours in LDS: level lv of thread t at lfr[lv * kBlock + t]
 // (16-byte records, so a wave's ds_read_b128 covers 1 KiB contiguously and is
 // bank-conflict free).
+template <int kThreads>
 struct LdsFrames {
   FrameC* base;  // already offset by threadIdx.x
-  __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kBlock]; }
+  __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kThreads]; }
 };
 
-// Wave-wide reductions with DPP (all 64 lanes must be active: the converged
-// loop of trace_sample_cv guarantees it at every call site).
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(
-      __builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), kCtrl, kRowMask, 0xF, false));
-}
-struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
-template <class Op>
-__device__ __forceinline__ float wave_reduce(float v) {
-  Op op;
-  v = op(v, dpp_f<0xB1, 0xF>(v));   // quad_perm [1,0,3,2]
-  v = op(v, dpp_f<0x4E, 0xF>(v));   // quad_perm [2,3,0,1]
-  v = op(v, dpp_f<0x141, 0xF>(v));  // row_half_mirror
-  v = op(v, dpp_f<0x140, 0xF>(v));  // row_mirror: every lane holds its row's result
-  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 15));
-  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 31));
-  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 47));
-  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-  return op(op(r0, r1), op(r2, r3));
-}
-
-template <class MatPtr, bool kDiag = false>
+template <class MatPtr, bool kDiag = false, int kThreads = kBlock>
 struct DevScene {
   FrameC* lfr;
-  __device__ __forceinline__ bool any(bool b) const { return __ballot(b) != 0ull; }
-  __device__ __forceinline__ float wave_max(float v) const { return wave_reduce<OpMax>(v); }
-  __device__ __forceinline__ int first_lane(bool b) const {
-    const uint64_t m = __ballot(b);
-    return m ? (int)__builtin_ctzll(m) : -1;
-  }
-  __device__ __forceinline__ float read_lane(float v, int l) const {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-  }
-  // bit k (k < min(n, 64)) = pred(k), evaluated by lane k.
   __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
-  template <class F>
-  __device__ __forceinline__ uint64_t sphere_mask(F pred) const {
-    const unsigned lane = threadIdx.x & 63u;
-    const bool p = (lane < n) ? pred(lane) : false;
-    return __ballot(p);
+  __device__ __forceinline__ LdsFrames<kThreads> frames() const {
+    return LdsFrames<kThreads>{lfr};
   }
-  __device__ __forceinline__ LdsFrames frames() const { return LdsFrames{lfr}; }
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
   mutable unsigned long long acc[kProbeSlots];
@@ -169,6 +134,9 @@ struct DevScene {
   }
 };
 
+struct KernelArgs;
+typedef void (*TraceFn)(const KernelArgs);
+
 struct KernelArgs {
   const float4* geom;
   const float* crad2;
@@ -180,6 +148,8 @@ struct KernelArgs {
   const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
   float* dst;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
+  unsigned* queue;           // tile counter of the work-queue kernel (variant 10), zeroed
+  uint4* timeline;           // per-wave records (variant 13) or null
 };
 
 __device__ __forceinline__ float canon_nan(float v) {
@@ -194,30 +164,23 @@ __device__ __forceinline__ float canon_nan(float v) {
 template <int S, int kVariant>
 struct MinWaves {
   static constexpr int value =
-      ((kVariant % 100 == 0 && S <= 6) || kVariant % 100 == 9) ? 7 : 1;
+      (((kVariant % 100 == 0 || kVariant % 100 >= 10) && S <= 6) || kVariant % 100 == 9) ? 7
+                                                                                         : 1;
 };
 
-template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_kernel(
-    const KernelArgs a) {
-  // LDS image: per-lane frame colours ((S-1) x kBlock x 16 B), then, when
-  // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
+// Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
+template <int S, bool kLds, int kThreads, class Sc>
+__device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   extern __shared__ float4 lds4[];
-  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  constexpr bool kDiag = kVariant >= 100;
-  constexpr int kBase = kDiag ? kVariant - 100 : kVariant;
   constexpr int NF = (S > 1) ? (S - 1) : 1;
-  DevScene<MatPtr, kDiag> sc;
-  if constexpr (kDiag)
-    for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
   sc.lfr = reinterpret_cast<FrameC*>(lds4) + threadIdx.x;
-  float4* sceneLds = lds4 + NF * kBlock;
+  float4* sceneLds = lds4 + NF * kThreads;
   if constexpr (kLds) {
     float* lmats = reinterpret_cast<float*>(sceneLds);
     const unsigned nm = (a.n + 1) * 8;
-    for (unsigned i = threadIdx.x; i < nm; i += kBlock) lmats[i] = a.mats[i];
+    for (unsigned i = threadIdx.x; i < nm; i += kThreads) lmats[i] = a.mats[i];
     float4* lg = sceneLds + (a.n + 1) * 2;
-    for (unsigned i = threadIdx.x; i < a.n4; i += kBlock)
+    for (unsigned i = threadIdx.x; i < a.n4; i += kThreads)
       lg[i] = reinterpret_cast<const float4*>(a.geom)[i];
     __syncthreads();
     sc.mats = lmats;
@@ -232,9 +195,18 @@ __global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_
   sc.n = a.n;
   sc.m = a.m;
   sc.n4 = a.n4;
-  const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const unsigned x = blockIdx.x * kTileW + (wave & 1u) * 8u + (lane & 7u);
-  const unsigned lr = blockIdx.y * kTileH + (wave >> 1) * 8u + (lane >> 3);
+}
+
+// One 8 x 8 pixel tile per wave: tile (tx, ty) of the shard's local rows.
+// Entered with the whole wave converged.
+template <int S, int kVariant, class Sc>
+__device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned tx,
+                                           unsigned ty) {
+  constexpr bool kDiag = kVariant >= 100;
+  constexpr int kBase = kDiag ? kVariant - 100 : kVariant;
+  const unsigned lane = threadIdx.x & 63u;
+  const unsigned x = tx * 8u + (lane & 7u);
+  const unsigned lr = ty * 8u + (lane >> 3);
   const bool valid = x < a.W && lr < a.rowsLocal;
   const unsigned gy = !valid ? 0u
                      : a.rowList ? a.rowList[lr]
@@ -245,7 +217,7 @@ __global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_
   // per lane against that bundle, then a ballot (see primary_sphere_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if constexpr (kBase == 0 || kBase == 7 || kBase == 8 || kBase == 9) {
+  if constexpr (kBase == 0 || kBase == 8 || kBase == 9 || kBase >= 10) {
     if (a.n <= 64) {
       float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
       if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
@@ -265,23 +237,22 @@ __global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_
       usePrim = true;
     }
   }
-  if constexpr (kBase != 7) {
-    if (!valid) return;
-  }
+  if (!valid) return;
   V3 pix;
   unsigned long long tk0 = 0;
-  if constexpr (kDiag) tk0 = __builtin_amdgcn_s_memtime();
-  if constexpr (kBase == 0) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
+  if constexpr (kDiag) {
+    for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
+    tk0 = __builtin_amdgcn_s_memtime();
+  }
+  if constexpr (kBase == 0 || kBase == 9 || kBase >= 10)
+    pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
   else if constexpr (kBase == 8) pix = shade_pixel<S, 3, true>(sc, a.cam, x, gy, usePrim, primSel);
-  else if constexpr (kBase == 9) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
-  else if constexpr (kBase == 7) pix = shade_pixel_cv<S>(sc, a.cam, x, gy, valid, usePrim, primSel);
   else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
   else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
   else if constexpr (kBase == 2) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
   else if constexpr (kBase == 3) pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
   else pix = shade_pixel_nodes<S, 2>(sc, a.cam, x, gy);
-  if (!valid) return;  // (variant 7 keeps every lane until here)
   if constexpr (kDiag) {
     sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
     // one wave-level add per slot (values are wave-uniform: s_memtime is scalar)
@@ -292,6 +263,144 @@ __global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_
   o[0] = canon_nan(pix.x);
   o[1] = canon_nan(pix.y);
   o[2] = canon_nan(pix.z);
+}
+
+// Threads per workgroup of a variant: 4 waves (2 x 2 tiles) by default; one
+// wave (variant 11) or two (variant 12) so a wave's slot is released as soon
+// as that wave (or its pair) is done instead of with the slowest of four.
+template <int kVariant>
+struct BlockThreads {
+  static constexpr int value = (kVariant % 100 == 11) ? 64 : (kVariant % 100 == 12) ? 128 : 256;
+};
+
+// One launch covers the frame; wave w of workgroup (bx, by) takes tile
+// (bx * TW + w % TW, by * TH + w / TW) with TW x TH = 2 x 2, 2 x 1 or 1 x 1.
+template <int S, bool kLds, int kVariant>
+__global__ __launch_bounds__(BlockThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
+void trace_kernel(const KernelArgs a) {
+  // LDS image: per-lane frame colours ((S-1) x threads x 16 B), then, when
+  // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
+  constexpr int kThreads = BlockThreads<kVariant>::value;
+  constexpr unsigned TW = kThreads >= 128 ? 2u : 1u, TH = kThreads == 256 ? 2u : 1u;
+  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
+  DevScene<MatPtr, (kVariant >= 100), kThreads> sc;
+  stage_scene<S, kLds, kThreads>(a, sc);
+  const unsigned wave = threadIdx.x >> 6;
+  unsigned t0 = 0;
+  if constexpr (kVariant == 13) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+  trace_tile<S, kVariant>(a, sc, blockIdx.x * TW + (wave % TW), blockIdx.y * TH + (wave / TW));
+  if constexpr (kVariant == 13) {
+    const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
+    // HW_ID (hwreg 4, 32 bits) and XCC_ID (hwreg 20, 16 bits) of this wave
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
+    if ((threadIdx.x & 63u) == 0) {
+      const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + wave;
+      a.timeline[w] = make_uint4(t0, t1, hw, xcc);
+    }
+  }
+}
+
+// Sample-parallel form (variant 14): each lane traces ONE primary sample, so
+// a wave takes floor(64 / nAA^2) consecutive pixels (7 at 3 x 3) with their
+// samples in lane order, instead of 64 pixels x all their samples.  A heavy
+// region (deep refraction trees) is then spread over nAA^2 times as many
+// waves, which keeps the frame's last waves short (the default kernel's
+// 8 x 8 tiles of 9 samples ran up to 3 ms each on C3), and a
+// wave's primary-ray bundle is a few pixels wide, so the cull is tighter.
+// Each pixel's sum is formed in the reference's sample order
+// (main.cpp:411-452: pix += c_s * inv for s = 0 .. nAA^2-1) by its first lane
+// from the other lanes' values (ds_bpermute moves the bits unchanged).
+// Requires nAA^2 <= 64; the host launches the default kernel otherwise.
+template <int S, bool kLds, int kVariant>
+__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_samples_kernel(
+    const KernelArgs a) {
+  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
+  DevScene<MatPtr, false, kBlock> sc;
+  stage_scene<S, kLds, kBlock>(a, sc);
+  const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const unsigned nAA = (unsigned)a.cam.nAA;
+  const unsigned SP = nAA * nAA;
+  const unsigned PPW = 64u / SP;
+  const unsigned pl = lane / SP, s = lane - pl * SP;
+  const size_t gw = (size_t)blockIdx.x * (kBlock / 64) + wave;
+  const size_t p = gw * PPW + pl;
+  const size_t total = (size_t)a.W * a.rowsLocal;
+  const bool valid = pl < PPW && p < total;
+  unsigned x = 0, lr = 0, gy = 0;
+  if (valid) {
+    lr = (unsigned)(p / a.W);
+    x = (unsigned)(p - (size_t)lr * a.W);
+    gy = a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
+  }
+  const int si = (int)(s / nAA), sj = (int)(s - (unsigned)si * nAA);
+  float rx, ry;
+  const V3 dir = sample_dir(a.cam, x, gy, si, sj, rx, ry);
+
+  // Primary-ray cull over the wave's sample directions (wave converged).
+  uint64_t primSel = ~0ull;
+  bool usePrim = false;
+  if (a.n <= 64) {
+    float x0 = valid ? rx : 3.0e38f, x1 = valid ? rx : -3.0e38f;
+    float y0 = valid ? ry : 3.0e38f, y1 = valid ? ry : -3.0e38f;
+    for (int off = 32; off > 0; off >>= 1) {
+      x0 = fminf(x0, __shfl_xor(x0, off));
+      x1 = fmaxf(x1, __shfl_xor(x1, off));
+      y0 = fminf(y0, __shfl_xor(y0, off));
+      y1 = fmaxf(y1, __shfl_xor(y1, off));
+    }
+    bool possible = false;
+    if (lane < a.n) {
+      const float4 g = sc.lgeom[lane];
+      possible = primary_sphere_possible(v3(g.x, g.y, g.z), sqrtf(g.w), x0, x1, y0, y1,
+                                         a.cam.zoom);
+    }
+    primSel = __ballot(possible);
+    usePrim = true;
+  }
+  V3 c = v3(0.f, 0.f, 0.f);
+  if (valid) {
+    c = trace_sample<S, 2>(sc, dir, sc.frames(), usePrim, primSel);
+    c = vsmul(a.cam.inv, c);
+  }
+  // Ordered per-pixel sum (whole wave converged again).
+  const unsigned base = pl * SP;
+  V3 pix = v3(0.f, 0.f, 0.f);
+  for (unsigned k = 0; k < SP; ++k) {
+    const int src = (int)((base + k) & 63u);
+    pix.x = pix.x + __shfl(c.x, src);
+    pix.y = pix.y + __shfl(c.y, src);
+    pix.z = pix.z + __shfl(c.z, src);
+  }
+  if (valid && s == 0) {
+    float* o = a.dst + ((size_t)lr * a.W + x) * 3;
+    o[0] = canon_nan(pix.x);
+    o[1] = canon_nan(pix.y);
+    o[2] = canon_nan(pix.z);
+  }
+}
+
+// Work-queue form (variant 10): a grid sized to the resident capacity, whose
+// waves each take the next 8 x 8 tile from a device counter until the frame
+// is exhausted.  A wave's slot is never held idle by slower waves of its
+// workgroup, and the frame's last tiles are shared out as waves free up.
+// Every wave leaves the loop once the counter passes the tile count.
+template <int S, bool kLds, int kVariant>
+__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_queue_kernel(
+    const KernelArgs a) {
+  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
+  DevScene<MatPtr, (kVariant >= 100)> sc;
+  stage_scene<S, kLds, kBlock>(a, sc);
+  const unsigned tilesX = (a.W + 7u) / 8u;
+  const unsigned tiles = tilesX * ((a.rowsLocal + 7u) / 8u);
+  const unsigned lane = threadIdx.x & 63u;
+  for (;;) {
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(a.queue, 1u);
+    t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+    if (t >= tiles) break;
+    trace_tile<S, kVariant>(a, sc, t % tilesX, t / tilesX);
+  }
 }
 
 // algebra.h:68-91 on the device: values are compared as floats (NaN never
@@ -333,7 +442,6 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
     out[i] = ppm_byte(c[i], m);
 }
 
-typedef void (*TraceFn)(const KernelArgs);
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
 //   0 (default) per-sample recursion + two-pass candidate-mask queries
 //   1 per-sample recursion, one sphere per step (first kernel)
@@ -342,13 +450,23 @@ typedef void (*TraceFn)(const KernelArgs);
 //   4 node-persistent: samples chained in one node loop + candidate masks
 //   5 as 0 but frame colours in private memory instead of LDS
 //   6 as 0 without the per-wave primary-ray sphere cull
-//   7 converged per-sample loop with per-query bundle culling (trace_sample_cv)
+//   (7, a converged loop with per-query bundle culls, was removed: DESIGN.md)
 //   8 as 0 with the tuned two-pass query (prefetched groups, uniform quotient path)
 //   9 as 0 compiled for 7 waves/SIMD (__launch_bounds__ min waves 7: <= 72 VGPRs)
+//   10 as 0 in the work-queue kernel (resident grid, waves pull 8 x 8 tiles)
+//   11 as 0 with one-wave workgroups (8 x 8 pixels)
+//   12 as 0 with two-wave workgroups (16 x 8 pixels)
+//   13 as 0 recording a per-wave timeline (rtg_diag_timeline)
+//   14 sample-parallel: one primary sample per lane (trace_samples_kernel)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
-  return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
+  if constexpr (V % 100 == 10)
+    return lds ? trace_queue_kernel<S, true, V> : trace_queue_kernel<S, false, V>;
+  else if constexpr (V == 14)
+    return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
+  else
+    return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
 }
 template <int S>
 static TraceFn trace_fn(bool lds, int variant) {
@@ -359,11 +477,15 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 4: return trace_fn_v<S, 4>(lds);
     case 5: return trace_fn_v<S, 5>(lds);
     case 6: return trace_fn_v<S, 6>(lds);
-    case 7: return trace_fn_v<S, 7>(lds);
     case 8: return trace_fn_v<S, 8>(lds);
     case 9: return trace_fn_v<S, 9>(lds);
+    case 10: return trace_fn_v<S, 10>(lds);
+    case 11: return trace_fn_v<S, 11>(lds);
+    case 12: return trace_fn_v<S, 12>(lds);
+    case 13: return trace_fn_v<S, 13>(lds);
+    case 14: return trace_fn_v<S, 14>(lds);
+    case 110: return trace_fn_v<S, 110>(lds);
     case 108: return trace_fn_v<S, 108>(lds);
-    case 107: return trace_fn_v<S, 107>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
     default: return trace_fn_v<S, 0>(lds);
@@ -392,6 +514,16 @@ struct rtg_context {
   float* lights = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
+  // Work-queue kernel: a ring of tile counters (one per launch, so launches on
+  // different streams do not share one) and the resident grid size per kernel.
+  static constexpr unsigned kQueueSlots = 64;
+  unsigned* queue = nullptr;
+  unsigned queueNext = 0;
+  uint4* timeline = nullptr;  // variant 13 records
+  size_t timelineCap = 0, timelineCount = 0;
+  rtg::TraceFn occFn = nullptr;
+  size_t occLds = 0;
+  unsigned occBlocks = 0;
   rtg_launch_opts opts{};
   bool hasScene = false;
 };
@@ -481,6 +613,8 @@ int rtg_context_destroy(rtg_context* ctx) {
   free_scene(ctx);
   (void)hipFree(ctx->maxScratch);
   (void)hipFree(ctx->diag);
+  (void)hipFree(ctx->queue);
+  (void)hipFree(ctx->timeline);
   delete ctx;
   return RTG_OK;
 }
@@ -496,6 +630,18 @@ int rtg_diag_read(rtg_context* ctx, unsigned long long* out, int reset) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, ctx->diag, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   if (reset) HIP_TRY(hipMemset(ctx->diag, 0, 8 * sizeof(unsigned long long)));
+  return RTG_OK;
+}
+
+int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* count) {
+  rtg_clear_error();
+  if (!ctx || (cap && !out4) || !count) return RTG_ERR_INVALID;
+  *count = ctx->timelineCount;
+  const size_t k = cap < ctx->timelineCount ? cap : ctx->timelineCount;
+  if (k == 0) return RTG_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out4, ctx->timeline, k * sizeof(uint4), hipMemcpyDeviceToHost));
   return RTG_OK;
 }
 
@@ -553,14 +699,17 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     return RTG_ERR_INVALID;
   }
   const bool ldsMats = ctx->n + 1 <= kLdsMatMax;
-  TraceFn fn = pick_trace(stackSize, ldsMats, ctx->opts.variant);
+  KernelArgs a;
+  int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
+  if (rc) return rc;
+  int variant = ctx->opts.variant;
+  // sample-parallel kernel: needs all of a pixel's samples in one wave
+  if (variant == 14 && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = 0;
+  TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {
     rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
     return RTG_ERR_INVALID;
   }
-  KernelArgs a;
-  int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
-  if (rc) return rc;
   unsigned rows;
   if (rowList) {
     rows = nRowList;
@@ -591,7 +740,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.rowList = rowList;
   a.dst = reinterpret_cast<float*>(dstDevice);
   a.diag = nullptr;
-  if (ctx->opts.variant >= 100) {
+  a.queue = nullptr;
+  a.timeline = nullptr;
+  if (variant >= 100) {
     if (!ctx->diag) {
       HIP_TRY(hipMalloc(&ctx->diag, 8 * sizeof(unsigned long long)));
       HIP_TRY(hipMemset(ctx->diag, 0, 8 * sizeof(unsigned long long)));
@@ -599,12 +750,56 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     a.diag = ctx->diag;
   }
   HIP_TRY(hipSetDevice(ctx->device));
-  dim3 grid((width + kTileW - 1) / kTileW, (rows + kTileH - 1) / kTileH);
-  const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * kBlock * 16;
+  const int vb = variant % 100;
+  const unsigned threads = vb == 11 ? 64u : vb == 12 ? 128u : (unsigned)kBlock;
+  const unsigned tw = threads >= 128 ? 16u : 8u, th = threads == 256 ? 16u : 8u;
+  dim3 grid((width + tw - 1) / tw, (rows + th - 1) / th);
+  if (variant == 14) {
+    const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);
+    const size_t waves = ((size_t)width * rows + ppw - 1) / ppw;
+    const size_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
+    if (blocks > 0x7FFFFFFFu) {
+      rtg_set_error("render: frame too large (%zu workgroups)", blocks);
+      return RTG_ERR_INVALID;
+    }
+    grid = dim3((unsigned)blocks, 1);
+  }
+  const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * threads * 16;
   const size_t lds = frameLds + (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) +
                                             (size_t)ctx->n4 * 16)
                                          : 0);
-  hipLaunchKernelGGL(fn, grid, dim3(kBlock), lds, (hipStream_t)stream, a);
+  if (variant % 100 == 10) {
+    if (!ctx->queue) {
+      HIP_TRY(hipMalloc(&ctx->queue, rtg_context::kQueueSlots * sizeof(unsigned)));
+    }
+    if (ctx->occFn != fn || ctx->occLds != lds) {
+      int perCU = 0, dev = ctx->device;
+      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void*)fn, kBlock, lds));
+      hipDeviceProp_t p;
+      HIP_TRY(hipGetDeviceProperties(&p, dev));
+      ctx->occFn = fn;
+      ctx->occLds = lds;
+      ctx->occBlocks = (unsigned)(perCU > 0 ? perCU : 1) * (unsigned)p.multiProcessorCount;
+    }
+    const unsigned tiles = ((width + 7u) / 8u) * ((rows + 7u) / 8u);
+    const unsigned need = (tiles + 3u) / 4u;  // 4 waves per workgroup
+    a.queue = ctx->queue + (ctx->queueNext++ % rtg_context::kQueueSlots);
+    HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(unsigned), (hipStream_t)stream));
+    grid = dim3(need < ctx->occBlocks ? need : ctx->occBlocks, 1);
+  }
+  if (variant == 13) {
+    const size_t waves = (size_t)grid.x * grid.y * (threads / 64);
+    if (ctx->timelineCap < waves) {
+      (void)hipFree(ctx->timeline);
+      ctx->timeline = nullptr;
+      ctx->timelineCap = 0;
+      HIP_TRY(hipMalloc(&ctx->timeline, waves * sizeof(uint4)));
+      ctx->timelineCap = waves;
+    }
+    ctx->timelineCount = waves;
+    a.timeline = ctx->timeline;
+  }
+  hipLaunchKernelGGL(fn, grid, dim3(threads), lds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());
   return RTG_OK;
 }

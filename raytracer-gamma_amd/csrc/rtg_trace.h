@@ -1102,319 +1102,6 @@ RTG_HD V3 shade_pixel_nodes(const Scene& sc, const Camera& cam, unsigned x, unsi
   return pix;
 }
 
-// ---------------------------------------------------------------------------
-// v7: converged per-sample loop with per-query bundle culling.
-//
-// All 64 lanes of a wave stay in the loop (finished lanes carry live=false), so
-// at the points marked "converged" the wave can reduce over its lanes: it
-// bounds the rays of the coming query and tests each sphere against that
-// bundle, one sphere per lane, to form a wave-uniform subset of spheres that
-// the query then runs over (closest_hit_sel / blocked_sel).  The tests are
-// conservative with wide margins (see primary_sphere_possible), so a sphere
-// left out cannot give a valid root: results are unchanged.
-//   * closest queries: origins in a ball (O, rho), unit directions within
-//     angle theta of an axis U;
-//   * shadow queries: segments from hit points in a ball (O, rho) to the
-//     light point L: a cone with apex L (plus a reach bound).
-// Scene interface used: any(bool), wave_min/max/sum(float) over the wave (the
-// host simulation is a wave of one lane), sphere_mask(pred) -> bit k = pred(k).
-
-// Subset of spheres that any ray of the bundle can reach with t > 0.  The
-// bundle is all rays from ball(O, rho) with unit directions within angle
-// theta of U (cosT, sinT given).  Keep iff angle(U, c - O) <= theta + alpha,
-// alpha = asin(rr / |c - O|): compared through cos(theta + alpha) =
-// cosT cos(alpha) - sinT sin(alpha), minus a 2e-3 margin (cos is
-// 1-Lipschitz, so that covers an angle margin of 2e-3 rad).
-RTG_HD bool bundle_sphere_possible(V3 c, float r, V3 O, float rho, V3 U, float cosT,
-                                   float sinT) {
-  const V3 v = vsub(c, O);
-  const float L2 = vdot(v, v);
-  const float rr = (r + rho) * 1.001f + 1.0e-3f;
-  if (!(L2 > rr * rr * 1.002f)) return true;
-  const float L = sqrtf(L2);
-  const float sa = rr / L;
-  const float ca = sqrtf(fmaxf(0.f, 1.f - sa * sa));
-  const float cl = cosT * ca - sinT * sa;  // cos(theta + alpha)
-  if (!(cl > -0.98f)) return true;          // theta + alpha near pi: keep
-  return vdot(U, v) >= (cl - 2.0e-3f) * L;
-}
-
-// Can sphere (c, r) meet a segment from a point of ball(O, rho) to the light
-// point Lp?  The segments lie in the cone with apex Lp, axis A = O - Lp and
-// half-angle beta = asin(rb / |A|) (sb, cb given), within distance |A| + rb of Lp.
-RTG_HD bool shadow_sphere_possible(V3 c, float r, V3 A, float DA, float rb, float sb, float cb,
-                                   V3 Lp) {
-  const V3 v = vsub(c, Lp);
-  const float L2 = vdot(v, v);
-  const float rr = r * 1.001f + 1.0e-3f;
-  if (!(L2 > rr * rr * 1.002f)) return true;
-  const float L = sqrtf(L2);
-  if (L - rr > (DA + rb) * 1.001f + 1.0e-3f) return false;  // beyond every segment's end
-  const float sa = rr / L;
-  const float ca = sqrtf(fmaxf(0.f, 1.f - sa * sa));
-  const float cl = cb * ca - sb * sa;
-  if (!(cl > -0.98f)) return true;
-  return vdot(A, v) >= (cl - 2.0e-3f) * (DA * L);
-}
-
-// Ball bounding the points p of participating lanes (converged call): centred
-// on the first participating lane's point, radius = one wave max-reduction.
-template <class Scene>
-RTG_HD bool wave_ball(const Scene& sc, bool part, V3 p, V3& O, float& rho) {
-  const bool ok = part && (p.x == p.x) && (p.y == p.y) && (p.z == p.z) &&
-                  fabsf(p.x) < 1e30f && fabsf(p.y) < 1e30f && fabsf(p.z) < 1e30f;
-  if (sc.any(part && !ok)) return false;
-  const int l0 = sc.first_lane(ok);
-  if (l0 < 0) return false;
-  O = v3(sc.read_lane(p.x, l0), sc.read_lane(p.y, l0), sc.read_lane(p.z, l0));
-  const V3 h = vsub(p, O);
-  rho = sqrtf(sc.wave_max(ok ? vdot(h, h) : 0.f)) * 1.001f;
-  return true;
-}
-
-// Spheres a bundle of closest-hit rays (o, d) of the `part` lanes can reach.
-template <class Scene>
-RTG_HD uint64_t closest_bundle_sel(const Scene& sc, bool part, V3 o, V3 d) {
-  const float dd = vdot(d, d);
-  // A zero or NaN direction has no valid root (a = 0 gives 0/0, NaN compares
-  // false), so such lanes are left out of the bounds; any other direction the
-  // bounds cannot handle disables the cull for this query.
-  const bool degenerate = part && !(dd != 0.f && dd == dd);
-  const bool ok = part && !degenerate && (dd > 1.0e-30f) && (dd < 1.0e30f);
-  if (sc.any(part && !degenerate && !ok)) return ~0ull;
-  V3 O;
-  float rho;
-  if (!wave_ball(sc, ok, o, O, rho)) return ~0ull;
-  const V3 u = ok ? vsmul(1.f / sqrtf(dd), d) : v3(0.f, 0.f, 0.f);
-  const int l0 = sc.first_lane(ok);
-  const V3 U = v3(sc.read_lane(u.x, l0), sc.read_lane(u.y, l0), sc.read_lane(u.z, l0));
-  const float cosT = fminf(1.f, -sc.wave_max(ok ? -vdot(u, U) : -2.f)) - 1.0e-4f;
-  if (!(cosT > 0.1f)) return ~0ull;  // bundle too wide to be worth a test
-  const float sinT = sqrtf(fmaxf(0.f, 1.f - cosT * cosT));
-  return sc.sphere_mask([&](unsigned k) {
-    float r2;
-    const V3 c = sc.sphere_lane(k, r2);
-    return bundle_sphere_possible(c, sqrtf(r2), O, rho, U, cosT, sinT);
-  });
-}
-
-// Shadow query restricted to the wave-uniform subset `sel` (spheres 0..63).
-template <class Scene>
-RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
-  const RayQ q = make_query(o, d);
-  uint64_t cand = 0;
-  for (uint64_t m = sel; m; m &= m - 1) {
-    const unsigned i = (unsigned)__builtin_ctzll(m);
-    float r2;
-    const V3 c = sc.sphere(i, r2);
-    const V3 disp = vsub(o, c);
-    const float b = 2.0f * vdot(d, disp);
-    const float cc = vdot(disp, disp) - r2;
-    const float rad = (b * b) - (q.a4 * cc);
-    cand |= (rad >= 0.0f) ? (1ull << i) : 0ull;
-  }
-  while (cand) {
-    const unsigned i = (unsigned)__builtin_ctzll(cand);
-    cand &= cand - 1;
-    float r2;
-    const V3 c = sc.sphere_lane(i, r2);
-    bool res;
-    const float t = ray_sphere(q, c, r2, res);
-    if (res && t < 1000.f) {
-      const V3 dist = vsmul(t, d);
-      if (vdot(dist, dist) < gap) return true;
-    }
-  }
-  return false;
-}
-
-template <int S, class Scene, class FStore>
-RTG_HD V3 trace_sample_cv(const Scene& sc, V3 dir0, FStore&& fc, bool active, bool usePrim,
-                          uint64_t primSel) {
-  constexpr int NF = (S > 1) ? (S - 1) : 1;
-  FrameR fr[NF];
-  int sp = 0;
-  V3 ret = v3(0.f, 0.f, 0.f);
-  V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
-  int rm = (int)sc.n;
-  bool live = active;
-  bool first = true;
-  const bool cull = sc.n <= 64;
-  while (sc.any(live)) {
-    // ---- closest query (raytracer.h:455), bundle-culled (converged here)
-    uint64_t sel = ~0ull;
-    sc.probe_begin(kProbePush);  // (slot reused: cull overhead in this variant)
-    if (cull) sel = (first && usePrim) ? primSel : closest_bundle_sel(sc, live, o, d);
-    sc.probe_end(kProbePush);
-    first = false;
-    float t = 1000.f;
-    int hit = -1;
-    sc.probe_begin(kProbeClosest);
-    if (live) hit = cull ? closest_hit_sel(sc, o, d, t, sel) : closest_hit_mask(sc, o, d, t);
-    sc.probe_end(kProbeClosest);
-
-    // ---- stage 0 shading (raytracer.h:454-550)
-    sc.probe_begin(kProbeShade);
-    const bool shade = live && hit >= 0 && significant(I);
-    if (live && hit < 0) ret = vmul(I, sc.mat(rm).matte);        // :544
-    V3 P = v3(0.f, 0.f, 0.f), N = v3(0.f, 0.f, 0.f);
-    Mat mh;
-    mh.matte = mh.gloss = v3(0.f, 0.f, 0.f);
-    mh.opacity = 0.f;
-    mh.refr = 1.f;
-    if (shade) {
-      float r2unused;
-      const V3 c = sc.sphere_lane((unsigned)hit, r2unused);
-      P = vadd(o, vsmul(t, d));
-      N = vnorm(vsub(P, c));
-      mh = sc.mat(hit);
-    }
-    // calculateMatte (raytracer.h:313-367) with shadow rays culled per light
-    const bool doMatte = shade && mh.opacity > 0.f;
-    V3 msum = v3(0.f, 0.f, 0.f);
-    if (sc.any(doMatte)) {
-      V3 O = v3(0.f, 0.f, 0.f);
-      float rho = 0.f;
-      sc.probe_begin(kProbePush);
-      const bool cullS = cull && wave_ball(sc, doMatte, P, O, rho);
-      sc.probe_end(kProbePush);
-      sc.probe_begin(kProbeMatte);
-      for (unsigned l = 0; l < sc.m; ++l) {
-        V3 Lpos, Lcol;
-        sc.light(l, Lpos, Lcol);
-        bool need = false;
-        V3 dir = v3(0.f, 0.f, 0.f);
-        float gap = 0.f, inc = 0.f;
-        if (doMatte) {
-          const V3 dist = vsub(Lpos, P);
-          gap = vdot(dist, dist);
-          dir = vsmul(1.f / rtg_sqrtf(gap), dist);
-          inc = vdot(N, dir);
-          need = inc > 0.f;
-        }
-        if (!sc.any(need)) continue;
-        uint64_t selL = ~0ull;
-        if (cullS) {
-          const V3 A = vsub(O, Lpos);
-          const float DA = sqrtf(vdot(A, A));
-          const float rb = rho * 1.001f + 1.0e-3f;
-          if (DA > rb * 1.01f) {
-            const float sb = rb / DA;
-            const float cb = sqrtf(fmaxf(0.f, 1.f - sb * sb));
-            selL = sc.sphere_mask([&](unsigned k) {
-              float r2;
-              const V3 c = sc.sphere_lane(k, r2);
-              return shadow_sphere_possible(c, sqrtf(r2), A, DA, rb, sb, cb, Lpos);
-            });
-          }
-        }
-        sc.probe_begin(kProbeShadow);
-        if (need) {
-          const bool blk = cull ? blocked_sel(sc, P, dir, gap, selL)
-                                : query_blocked<2>(sc, P, dir, gap);
-          if (!blk) msum = vadd(msum, vsmul(inc / gap, Lcol));
-        }
-        sc.probe_end(kProbeShadow);
-      }
-      sc.probe_end(kProbeMatte);
-    }
-
-    bool descended = false;
-    if (shade) {
-      const float op = mh.opacity;
-      const float tr = 1.f - op;
-      V3 colour = v3(0.f, 0.f, 0.f);
-      if (op > 0.f) {
-        V3 tmp = vmul(I, mh.matte);
-        tmp = vsmul(op, tmp);
-        tmp = vmul(msum, tmp);
-        colour = vadd(tmp, colour);
-      }
-      if (tr > 0.f) {
-        const bool leaf = (sp >= S - 1);
-        const Mat mr = sc.mat(rm);
-        V3 cdir;
-        float R;
-        sc.probe_begin(kProbeRefraction);
-        const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
-        sc.probe_end(kProbeRefraction);
-        const float prod = tr * R;
-        V3 rc = vsmul(prod, v3(1.f, 1.f, 1.f));
-        rc = vadd(rc, vsmul(mr.opacity, mh.gloss));
-        rc = vmul(I, rc);
-        const bool sigR = significant(rc);
-        if (!leaf) {
-          const int lv = sp < NF ? sp : NF - 1;
-          FrameC& f = fc(lv);
-          f.cx = colour.x; f.cy = colour.y; f.cz = colour.z;
-          f.meta = ((unsigned)rm << 2) | (sigR ? 2u : 0u);
-          if (sigR) {
-            const float perp = 2.f * vdot(d, N);
-            const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
-            fr[lv].rd = rd;
-            fr[lv].ro = vadd(P, vsmul(0.01f, rd));
-            fr[lv].rI = rc;
-          }
-          ++sp;
-          ret = colour;
-          I = vsmul((1.f - R), vsmul(tr, I));
-          o = P;
-          d = cdir;
-          rm = tgt;
-          descended = true;
-        } else {
-          const V3 c1 = vadd(colour, colour);
-          ret = sigR ? vadd(c1, c1) : c1;
-        }
-      } else {
-        ret = colour;
-      }
-    }
-    sc.probe_end(kProbeShade);
-    // ---- unwind (stages 1 and 2)
-    if (live && !descended) {
-      sc.probe_begin(kProbeUnwind);
-      bool descend = false;
-      while (sp > 0) {
-        const int lv = sp - 1 < NF ? sp - 1 : NF - 1;
-        FrameC& f = fc(lv);
-        const V3 fcol = vadd(ret, v3(f.cx, f.cy, f.cz));
-        ret = fcol;
-        if ((f.meta & 3u) == 2u) {
-          f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
-          f.meta = (f.meta & ~3u) | 1u;
-          o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 2);
-          descend = true;
-          break;
-        }
-        --sp;
-      }
-      sc.probe_end(kProbeUnwind);
-      if (!descend) live = false;
-    }
-  }
-  return ret;
-}
-
-template <int S, class Scene>
-RTG_HD V3 shade_pixel_cv(const Scene& sc, const Camera& cam, unsigned x, unsigned y, bool active,
-                         bool usePrim, uint64_t primSel) {
-  const float pxX = (((float)x - cam.halfW)) * cam.xs;
-  const float pxY = (cam.halfH - (float)y) * cam.ys;
-  V3 pix = v3(0.f, 0.f, 0.f);
-  for (int i = 0; i < cam.nAA; ++i) {
-    for (int j = 0; j < cam.nAA; ++j) {
-      const float rx = (pxX + (float)(((float)j) * cam.st)) * cam.asp;
-      const float ry = (pxY + (float)(((float)i) * cam.st));
-      const V3 dir = vnorm(v3(rx, ry, cam.zoom));
-      V3 c = trace_sample_cv<S>(sc, dir, sc.frames(), active, usePrim, primSel);
-      c = vsmul(cam.inv, c);
-      pix = vadd(pix, c);
-    }
-  }
-  return pix;
-}
-
 // Bounds of the primary-ray directions of pixel (x, y) (all its samples):
 // X = (pxX + j*st)*asp, Y = pxY + i*st for i, j in [0, nAA).
 RTG_HD void primary_bounds(const Camera& cam, unsigned x, unsigned y, float& x0, float& x1,
@@ -1427,6 +1114,17 @@ RTG_HD void primary_bounds(const Camera& cam, unsigned x, unsigned y, float& x0,
   x1 = fmaxf(a, b);
   y0 = fminf(pxY, pxY + ext);
   y1 = fmaxf(pxY, pxY + ext);
+}
+
+// The primary ray of sample (i, j) of pixel (x, y): the screen-plane point
+// (rx, ry) (main.cpp:419-426) and its normalised direction (main.cpp:428).
+RTG_HD V3 sample_dir(const Camera& cam, unsigned x, unsigned y, int i, int j, float& rx,
+                     float& ry) {
+  const float pxX = (((float)x - cam.halfW)) * cam.xs;
+  const float pxY = (cam.halfH - (float)y) * cam.ys;
+  rx = (pxX + (float)(((float)j) * cam.st)) * cam.asp;
+  ry = (pxY + (float)(((float)i) * cam.st));
+  return vnorm(v3(rx, ry, cam.zoom));
 }
 
 // main.cpp:411-452 for pixel (x, y) of the frame.

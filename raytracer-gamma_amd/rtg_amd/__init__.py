@@ -53,7 +53,7 @@ EXPORTED = [
     "rtg_last_error", "rtg_abi_version", "rtg_device_count", "rtg_device_info",
     "rtg_render", "rtg_context_create", "rtg_context_destroy", "rtg_context_set_scene",
     "rtg_shard_rows", "rtg_shard_global_row", "rtg_render_device", "rtg_render_rows_device",
-    "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read",
+    "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read", "rtg_diag_timeline",
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate",
 ]
@@ -90,6 +90,7 @@ def lib() -> ctypes.CDLL:
         L.rtg_render_rows.argtypes = [i, vp, u, vp, u, u, u, f, f, i, vp, u, vp]
         L.rtg_set_launch_opts.argtypes = [vp, vp]
         L.rtg_diag_read.argtypes = [vp, vp, i]
+        L.rtg_diag_timeline.argtypes = [vp, vp, sz, vp]
         L.rtg_max_colour.argtypes = [vp, sz]
         L.rtg_max_colour.restype = f
         L.rtg_max_colour_device.argtypes = [vp, vp, sz, vp, vp]
@@ -257,6 +258,14 @@ class Context:
         _check(lib().rtg_diag_read(self._h, ctypes.cast(out, ctypes.c_void_p), int(reset)),
                "rtg_diag_read")
         return [int(v) for v in out]
+
+    def diag_timeline(self, cap: int = 1 << 20) -> np.ndarray:
+        """Per-wave records {start, end, HW_ID, XCC_ID} of the last timeline-variant launch."""
+        out = np.zeros((cap, 4), np.uint32)
+        cnt = ctypes.c_size_t(0)
+        _check(lib().rtg_diag_timeline(self._h, ctypes.c_void_p(out.ctypes.data), cap,
+                                       ctypes.byref(cnt)), "rtg_diag_timeline")
+        return out[:min(cap, cnt.value)]
 
     def render_device(self, width, height, dst_ptr: int, zoom=-4.0, alias_factor=3.0,
                       stack_size=6, row_block=16, shard=0, n_shards=1, stream: int = 0):

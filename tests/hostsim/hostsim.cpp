@@ -34,17 +34,6 @@ struct HostScene {
     rtg::FrameC& operator()(int lv) const { return f[lv]; }
   };
   mutable rtg::FrameC fr[16];
-  bool any(bool b) const { return b; }
-  float wave_max(float v) const { return v; }
-  int first_lane(bool b) const { return b ? 0 : -1; }
-  float read_lane(float v, int) const { return v; }
-  template <class F>
-  uint64_t sphere_mask(F pred) const {
-    uint64_t m = 0;
-    for (unsigned k = 0; k < n && k < 64; ++k)
-      if (pred(k)) m |= 1ull << k;
-    return m;
-  }
   Frames frames() const { return Frames{fr}; }
   void probe_end(int) const {}
   void sphere4(unsigned i, rtg::V3* c, float* r2) const {
@@ -81,21 +70,15 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
       case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
       case 8: p = rtg::shade_pixel<S, 3, true>(sc, cam, x, y); break;
-      case 7: {
-        uint64_t sel = ~0ull;
-        bool use = sc.n <= 64;
-        if (use) {
-          float x0, x1, y0, y1;
-          rtg::primary_bounds(cam, x, y, x0, x1, y0, y1);
-          sel = 0;
-          for (unsigned k = 0; k < sc.n; ++k) {
-            float r2;
-            const rtg::V3 c = sc.sphere(k, r2);
-            if (rtg::primary_sphere_possible(c, sqrtf(r2), x0, x1, y0, y1, cam.zoom))
-              sel |= 1ull << k;
-          }
+      case 14: {  // sample-parallel kernel: samples traced one by one, summed in order
+        p = rtg::v3(0.f, 0.f, 0.f);
+        for (int s = 0; s < cam.nAA * cam.nAA; ++s) {
+          float rx, ry;
+          const rtg::V3 d = rtg::sample_dir(cam, x, y, s / cam.nAA, s % cam.nAA, rx, ry);
+          rtg::V3 c = rtg::trace_sample<S, 2>(sc, d, sc.frames());
+          c = rtg::vsmul(cam.inv, c);
+          p = rtg::vadd(p, c);
         }
-        p = rtg::shade_pixel_cv<S>(sc, cam, x, y, true, use, sel);
         break;
       }
       default: {

@@ -106,6 +106,35 @@ def test_random_scenes_vs_oracle(R, oracle):
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
 
 
+@pytest.mark.parametrize("variant", [14, 10])
+def test_random_scenes_vs_oracle_variants(R, oracle, torch_cuda, variant):
+    """Mapping variants over random scenes, sizes and alias factors (the
+    sample-parallel kernel packs 64 // nAA^2 pixels per wave and falls back to
+    the default kernel above nAA = 8)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77 + variant)
+    ctx = R.Context(0)
+    ctx.set_variant(variant)
+    for trial in range(16):
+        S = int(rng.integers(1, 17))
+        n, m = int(rng.integers(0, 20)), int(rng.integers(0, 5))
+        W, H = int(rng.integers(1, 70)), int(rng.integers(1, 50))
+        aa = float(rng.choice([0.5, 1.0, 2.0, 3.0, 2.5, 4.0, 5.0, 8.0, 9.0]))
+        zoom = float(rng.choice([-4.0, -2.0, 3.0]))
+        sph, lg = random_scene(rng, n, m)
+        if zoom > 0:
+            sph["pos"][:, 2] *= -1.0
+        want = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
+        ctx.set_scene(sph, lg)
+        out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ctx.render_device(W, H, out.data_ptr(), zoom=zoom, alias_factor=aa, stack_size=S,
+                          stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert bits_equal(got, want), (trial, S, n, m, W, H, aa, first_mismatch(got, want))
+    ctx.close()
+
+
 def test_large_scene_global_material_path(R, oracle):
     """n + 1 > 1025 materials: the kernel reads materials from global memory."""
     rng = np.random.default_rng(99)
@@ -135,6 +164,45 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
         torch.cuda.synchronize()
         fb = dist.assemble(buf, H, B).cpu().numpy()
         assert canon_md5(fb) == c["fb_md5"], G
+    ctx.close()
+
+
+@pytest.mark.parametrize("variant", [10, 11, 12, 14])
+def test_queue_kernel_full_frames(R, golden, torch_cuda, variant):
+    """The work-queue kernel over whole frames, sharded frames, row lists and
+    back-to-back launches on two streams (each launch has its own counter)."""
+    from rtg_amd import dist
+    torch = torch_cuda
+    ctx = R.Context(0)
+    ctx.set_variant(variant)
+    for name in ["c1", "c3"]:
+        c = golden["configs"][name]
+        sph, lg = load_scene(name, c["spheres"], c["lights"])
+        W, H, S = c["W"], c["H"], c["stack_size"]
+        ctx.set_scene(sph, lg)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        a = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        b = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        for _ in range(2):
+            ctx.render_device(W, H, a.data_ptr(), stack_size=S, stream=s1.cuda_stream)
+            ctx.render_device(W, H, b.data_ptr(), stack_size=S, stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+        assert canon_md5(a.cpu().numpy()) == c["fb_md5"], name
+        assert canon_md5(b.cpu().numpy()) == c["fb_md5"], name
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    W, H, S, B, G = c["W"], c["H"], c["stack_size"], 16, 3
+    ctx.set_scene(sph, lg)
+    Rmax = dist.padded_rows(H, B, G)
+    buf = torch.zeros((G, Rmax, W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for g in range(G):
+        rows = torch.tensor(R.shard_row_indices(H, B, g, G), dtype=torch.int32, device="cuda")
+        ctx.render_rows_device(W, H, rows.data_ptr(), rows.numel(), buf[g].data_ptr(),
+                               stack_size=S, stream=stream)
+    torch.cuda.synchronize()
+    fb = dist.assemble(buf, H, B).cpu().numpy()
+    assert canon_md5(fb) == c["fb_md5"]
     ctx.close()
 
 
@@ -179,7 +247,7 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 100, 107, 108])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 100, 108, 110])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda

@@ -19,3 +19,4 @@ for grp in "${GRPS[@]}"; do
      -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/pmc_$TAG/p$i.json 2> $OUT/pmc_$TAG/p$i.err || { echo "pass $i failed"; tail -5 $OUT/pmc_$TAG/p$i.err; exit 1; }
 done
 echo "== done"
+python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT/pmc_$TAG --json $OUT/pmc_$TAG/pmc_c3.json > $OUT/pmc_$TAG/summary.txt && cat $OUT/pmc_$TAG/summary.txt

@@ -1,24 +1,64 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_pmc.sh output: per-counter average over the trace kernel's dispatches."""
+"""Summarise tools/gpu_pmc.sh output: per-counter average over the trace
+kernel's dispatches, HBM traffic per launch (MI355X_MICROARCH.md: FETCH_SIZE
+reads 1/2 of a wide coalesced stream on gfx950, so it is doubled; WRITE_SIZE
+as is; both in KiB), and optionally a JSON record for bench.py.
+
+  python tools/pmc_summary.py gpurun_out/pmc_TAG [--json profiles/pmc_c3.json]
+"""
+import argparse
 import collections
 import csv
 import glob
+import hashlib
+import json
 import os
-import sys
 
-d = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "trace_kernel"
-agg = collections.defaultdict(list)
-for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
-    for r in csv.DictReader(open(f)):
-        if kern in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-avg = {k: sum(v) / len(v) for k, v in agg.items()}
-for k in sorted(avg):
-    print(f"{k:28s} {avg[k]:.6g}  (n={len(agg[k])})")
-if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
-    print("VALU lane utilisation       %.3f" % (avg["SQ_THREAD_CYCLES_VALU"] / (avg["SQ_ACTIVE_INST_VALU"] * 64)))
-if "FETCH_SIZE" in avg:
-    print("HBM read  (FETCH_SIZE x2, gfx950 correction) %.1f MB" % (avg["FETCH_SIZE"] * 2 * 1024 / 1e6))
-if "WRITE_SIZE" in avg:
-    print("HBM write (WRITE_SIZE)                       %.1f MB" % (avg["WRITE_SIZE"] * 1024 / 1e6))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = ["raytracer-gamma_amd/csrc/rtg_trace.h", "raytracer-gamma_amd/csrc/rtg_kernel.hip"]
+
+
+def source_md5():
+    h = hashlib.md5()
+    for f in SRC:
+        h.update(open(os.path.join(ROOT, f), "rb").read())
+    return h.hexdigest()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", default="trace_kernel")
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--variant", type=int, default=0)
+    a = ap.parse_args()
+    agg = collections.defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if a.kernel in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    avg = {k: sum(v) / len(v) for k, v in agg.items()}
+    for k in sorted(avg):
+        print(f"{k:28s} {avg[k]:.6g}  (n={len(agg[k])})")
+    out = {"config": a.config, "variant": a.variant, "kernel": a.kernel,
+           "source_md5": source_md5(), "counters": avg}
+    if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
+        u = avg["SQ_THREAD_CYCLES_VALU"] / (avg["SQ_ACTIVE_INST_VALU"] * 64)
+        out["valu_lane_utilisation"] = u
+        print("VALU lane utilisation       %.3f" % u)
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        rd = avg["FETCH_SIZE"] * 2 * 1024
+        wr = avg["WRITE_SIZE"] * 1024
+        out["hbm_read_bytes"] = rd
+        out["hbm_write_bytes"] = wr
+        out["traffic_bytes"] = rd + wr
+        print("HBM read  (FETCH_SIZE x2, gfx950 correction) %.1f MB" % (rd / 1e6))
+        print("HBM write (WRITE_SIZE)                       %.1f MB" % (wr / 1e6))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+        print("wrote", a.json)
+
+
+if __name__ == "__main__":
+    main()
