@@ -129,14 +129,16 @@ int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
 /* Launch-configuration knobs (performance only; results never change). */
 typedef struct rtg_launch_opts {
   int variant;        /* 0 = default kernel; other values select A/B variants */
-  int reserved[7];
+  int flags;          /* RTG_LAUNCH_* bits */
+  int reserved[6];
 } rtg_launch_opts;
 int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts);
 /* Diagnostic variants (variant >= 100) sum per-wave s_memtime cycles spent in
  * {closest-hit queries, shadow queries, refraction, whole pixel} into 8
  * counters; read (and optionally zero) them.  Zeros for normal variants. */
 int rtg_diag_read(rtg_context* ctx, unsigned long long* out8, int reset);
-/* Wave timeline of the last launch of the timeline variant (13): one record
+#define RTG_LAUNCH_TIMELINE 1 /* record a per-wave timeline (rtg_diag_timeline) */
+/* Wave timeline of the last launch made with RTG_LAUNCH_TIMELINE: one record
  * per wave {start, end (s_memrealtime, 100 MHz, low 32 bits), HW_ID, XCC_ID},
  * in launch order.  Copies min(cap, waves) records; *count = waves recorded.
  * Diagnostic only (occupancy analysis, tools/timeline.py). */

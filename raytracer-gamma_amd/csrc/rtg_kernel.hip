@@ -148,8 +148,7 @@ struct KernelArgs {
   const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
   float* dst;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
-  unsigned* queue;           // tile counter of the work-queue kernel (variant 10), zeroed
-  uint4* timeline;           // per-wave records (variant 13) or null
+  uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
 };
 
 __device__ __forceinline__ float canon_nan(float v) {
@@ -158,14 +157,13 @@ __device__ __forceinline__ float canon_nan(float v) {
 }
 
 // Minimum waves per SIMD requested from the register allocator: 7 (<= 72
-// VGPRs) where the LDS image of S-1 frame levels still admits 7 workgroups
-// per CU (S <= 6 with a small scene); measured +1-2 % over the unconstrained
-// 78-VGPR build at 6 waves/SIMD (C3).  Variant 9 forces it for any S.
+// VGPRs) where the LDS image of S-1 frame levels still admits 7 waves per
+// SIMD (S <= 6 with a small scene); measured +1-2 % over the unconstrained
+// 78-VGPR build at 6 waves/SIMD (C3, tile kernel).
 template <int S, int kVariant>
 struct MinWaves {
   static constexpr int value =
-      (((kVariant % 100 == 0 || kVariant % 100 >= 10) && S <= 6) || kVariant % 100 == 9) ? 7
-                                                                                         : 1;
+      ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant == 14) && S <= 6) ? 7 : 1;
 };
 
 // Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
@@ -217,7 +215,7 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
   // per lane against that bundle, then a ballot (see primary_sphere_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if constexpr (kBase == 0 || kBase == 8 || kBase == 9 || kBase >= 10) {
+  if constexpr (kBase == 0 || kBase == 8 || kBase == 9) {
     if (a.n <= 64) {
       float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
       if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
@@ -244,7 +242,7 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
     for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
     tk0 = __builtin_amdgcn_s_memtime();
   }
-  if constexpr (kBase == 0 || kBase == 9 || kBase >= 10)
+  if constexpr (kBase == 0 || kBase == 9)
     pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
   else if constexpr (kBase == 8) pix = shade_pixel<S, 3, true>(sc, a.cam, x, gy, usePrim, primSel);
@@ -265,40 +263,33 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
   o[2] = canon_nan(pix.z);
 }
 
-// Threads per workgroup of a variant: 4 waves (2 x 2 tiles) by default; one
-// wave (variant 11) or two (variant 12) so a wave's slot is released as soon
-// as that wave (or its pair) is done instead of with the slowest of four.
-template <int kVariant>
-struct BlockThreads {
-  static constexpr int value = (kVariant % 100 == 11) ? 64 : (kVariant % 100 == 12) ? 128 : 256;
-};
+// Timeline record of one wave (launch flag RTG_LAUNCH_TIMELINE): start/end
+// s_memrealtime (100 MHz), HW_ID (hwreg 4) and XCC_ID (hwreg 20).  Called
+// with the wave converged.
+__device__ __forceinline__ void record_wave(const KernelArgs& a, unsigned t0, size_t w) {
+  if (a.timeline == nullptr) return;
+  const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
+  if ((threadIdx.x & 63u) == 0) a.timeline[w] = make_uint4(t0, t1, hw, xcc);
+}
 
-// One launch covers the frame; wave w of workgroup (bx, by) takes tile
-// (bx * TW + w % TW, by * TH + w / TW) with TW x TH = 2 x 2, 2 x 1 or 1 x 1.
+// Tile kernels: one 8 x 8 pixel tile per wave, all samples of a pixel in its
+// lane; a workgroup is 2 x 2 tiles.
 template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(BlockThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
+__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value))
 void trace_kernel(const KernelArgs a) {
   // LDS image: per-lane frame colours ((S-1) x threads x 16 B), then, when
   // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
-  constexpr int kThreads = BlockThreads<kVariant>::value;
-  constexpr unsigned TW = kThreads >= 128 ? 2u : 1u, TH = kThreads == 256 ? 2u : 1u;
+  constexpr int kThreads = kBlock;
+  constexpr unsigned TW = 2u, TH = 2u;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
   DevScene<MatPtr, (kVariant >= 100), kThreads> sc;
   stage_scene<S, kLds, kThreads>(a, sc);
   const unsigned wave = threadIdx.x >> 6;
-  unsigned t0 = 0;
-  if constexpr (kVariant == 13) t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+  const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   trace_tile<S, kVariant>(a, sc, blockIdx.x * TW + (wave % TW), blockIdx.y * TH + (wave / TW));
-  if constexpr (kVariant == 13) {
-    const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
-    // HW_ID (hwreg 4, 32 bits) and XCC_ID (hwreg 20, 16 bits) of this wave
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
-    if ((threadIdx.x & 63u) == 0) {
-      const size_t w = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + wave;
-      a.timeline[w] = make_uint4(t0, t1, hw, xcc);
-    }
-  }
+  record_wave(a, t0, ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + wave);
 }
 
 // Sample-parallel form (variant 14): each lane traces ONE primary sample, so
@@ -312,18 +303,15 @@ void trace_kernel(const KernelArgs a) {
 // (main.cpp:411-452: pix += c_s * inv for s = 0 .. nAA^2-1) by its first lane
 // from the other lanes' values (ds_bpermute moves the bits unchanged).
 // Requires nAA^2 <= 64; the host launches the default kernel otherwise.
-template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_samples_kernel(
-    const KernelArgs a) {
-  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, false, kBlock> sc;
-  stage_scene<S, kLds, kBlock>(a, sc);
-  const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+// Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
+// rows, all their samples) traced by one wave, entered converged.
+template <int S, class Sc>
+__device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
+  const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned SP = nAA * nAA;
   const unsigned PPW = 64u / SP;
   const unsigned pl = lane / SP, s = lane - pl * SP;
-  const size_t gw = (size_t)blockIdx.x * (kBlock / 64) + wave;
   const size_t p = gw * PPW + pl;
   const size_t total = (size_t)a.W * a.rowsLocal;
   const bool valid = pl < PPW && p < total;
@@ -380,27 +368,24 @@ __global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_
   }
 }
 
-// Work-queue form (variant 10): a grid sized to the resident capacity, whose
-// waves each take the next 8 x 8 tile from a device counter until the frame
-// is exhausted.  A wave's slot is never held idle by slower waves of its
-// workgroup, and the frame's last tiles are shared out as waves free up.
-// Every wave leaves the loop once the counter passes the tile count.
+template <int kVariant>
+struct SampleThreads {
+  static constexpr int value = (kVariant == 14) ? kBlock : 64;
+};
+
+// One launch, one pixel group per wave: one-wave workgroups (default), or
+// four-wave ones (variant 14).
 template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value)) void trace_queue_kernel(
-    const KernelArgs a) {
+__global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
+void trace_samples_kernel(const KernelArgs a) {
+  constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100)> sc;
-  stage_scene<S, kLds, kBlock>(a, sc);
-  const unsigned tilesX = (a.W + 7u) / 8u;
-  const unsigned tiles = tilesX * ((a.rowsLocal + 7u) / 8u);
-  const unsigned lane = threadIdx.x & 63u;
-  for (;;) {
-    unsigned t = 0;
-    if (lane == 0) t = atomicAdd(a.queue, 1u);
-    t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
-    if (t >= tiles) break;
-    trace_tile<S, kVariant>(a, sc, t % tilesX, t / tilesX);
-  }
+  DevScene<MatPtr, false, kThreads> sc;
+  const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
+  stage_scene<S, kLds, kThreads>(a, sc);
+  const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  trace_group<S>(a, sc, gw);
+  record_wave(a, t0, gw);
 }
 
 // algebra.h:68-91 on the device: values are compared as floats (NaN never
@@ -443,27 +428,25 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 }
 
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
-//   0 (default) per-sample recursion + two-pass candidate-mask queries
+//   0 (default) sample-parallel: one primary sample per lane, one-wave
+//     workgroups (trace_samples_kernel); falls back to 9 when nAA > 8
 //   1 per-sample recursion, one sphere per step (first kernel)
 //   2 one-query-per-iteration state machine + candidate masks
 //   3 one-query-per-iteration state machine, four spheres per step
 //   4 node-persistent: samples chained in one node loop + candidate masks
-//   5 as 0 but frame colours in private memory instead of LDS
-//   6 as 0 without the per-wave primary-ray sphere cull
+//   5 as 9 but frame colours in private memory instead of LDS
+//   6 as 9 without the per-wave primary-ray sphere cull
 //   (7, a converged loop with per-query bundle culls, was removed: DESIGN.md)
-//   8 as 0 with the tuned two-pass query (prefetched groups, uniform quotient path)
-//   9 as 0 compiled for 7 waves/SIMD (__launch_bounds__ min waves 7: <= 72 VGPRs)
-//   10 as 0 in the work-queue kernel (resident grid, waves pull 8 x 8 tiles)
-//   11 as 0 with one-wave workgroups (8 x 8 pixels)
-//   12 as 0 with two-wave workgroups (16 x 8 pixels)
-//   13 as 0 recording a per-wave timeline (rtg_diag_timeline)
-//   14 sample-parallel: one primary sample per lane (trace_samples_kernel)
-//   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read)
+//   8 as 9 with the tuned two-pass query (prefetched groups, uniform quotient path)
+//   9 tile kernel: an 8 x 8 pixel tile per wave, each lane all samples of its
+//     pixel (per-sample recursion + two-pass candidate-mask queries + per-wave
+//     primary cull), 7 waves/SIMD; the default until the sample-parallel kernel
+//   14 as 0 with four-wave workgroups
+//   (10-12, 15, 16: work-queue and workgroup-size trials, removed: DESIGN.md)
+//   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
-  if constexpr (V % 100 == 10)
-    return lds ? trace_queue_kernel<S, true, V> : trace_queue_kernel<S, false, V>;
-  else if constexpr (V == 14)
+  if constexpr (V == 0 || V == 14)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -479,12 +462,7 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 6: return trace_fn_v<S, 6>(lds);
     case 8: return trace_fn_v<S, 8>(lds);
     case 9: return trace_fn_v<S, 9>(lds);
-    case 10: return trace_fn_v<S, 10>(lds);
-    case 11: return trace_fn_v<S, 11>(lds);
-    case 12: return trace_fn_v<S, 12>(lds);
-    case 13: return trace_fn_v<S, 13>(lds);
     case 14: return trace_fn_v<S, 14>(lds);
-    case 110: return trace_fn_v<S, 110>(lds);
     case 108: return trace_fn_v<S, 108>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
@@ -514,16 +492,8 @@ struct rtg_context {
   float* lights = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
-  // Work-queue kernel: a ring of tile counters (one per launch, so launches on
-  // different streams do not share one) and the resident grid size per kernel.
-  static constexpr unsigned kQueueSlots = 64;
-  unsigned* queue = nullptr;
-  unsigned queueNext = 0;
-  uint4* timeline = nullptr;  // variant 13 records
+  uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
   size_t timelineCap = 0, timelineCount = 0;
-  rtg::TraceFn occFn = nullptr;
-  size_t occLds = 0;
-  unsigned occBlocks = 0;
   rtg_launch_opts opts{};
   bool hasScene = false;
 };
@@ -613,7 +583,6 @@ int rtg_context_destroy(rtg_context* ctx) {
   free_scene(ctx);
   (void)hipFree(ctx->maxScratch);
   (void)hipFree(ctx->diag);
-  (void)hipFree(ctx->queue);
   (void)hipFree(ctx->timeline);
   delete ctx;
   return RTG_OK;
@@ -704,7 +673,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   if (rc) return rc;
   int variant = ctx->opts.variant;
   // sample-parallel kernel: needs all of a pixel's samples in one wave
-  if (variant == 14 && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = 0;
+  // sample-parallel kernels need all of a pixel's samples in one wave
+  if ((variant == 0 || variant == 14) && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = 9;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {
     rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
@@ -740,7 +710,6 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.rowList = rowList;
   a.dst = reinterpret_cast<float*>(dstDevice);
   a.diag = nullptr;
-  a.queue = nullptr;
   a.timeline = nullptr;
   if (variant >= 100) {
     if (!ctx->diag) {
@@ -750,14 +719,14 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     a.diag = ctx->diag;
   }
   HIP_TRY(hipSetDevice(ctx->device));
-  const int vb = variant % 100;
-  const unsigned threads = vb == 11 ? 64u : vb == 12 ? 128u : (unsigned)kBlock;
-  const unsigned tw = threads >= 128 ? 16u : 8u, th = threads == 256 ? 16u : 8u;
-  dim3 grid((width + tw - 1) / tw, (rows + th - 1) / th);
-  if (variant == 14) {
+  unsigned threads = (unsigned)kBlock;
+  dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
+  if (variant == 0 || variant == 14) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);
     const size_t waves = ((size_t)width * rows + ppw - 1) / ppw;
-    const size_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
+    const unsigned tpb = variant == 0 ? 64u : (unsigned)kBlock;
+    const size_t blocks = (waves + tpb / 64 - 1) / (tpb / 64);
+    threads = tpb;
     if (blocks > 0x7FFFFFFFu) {
       rtg_set_error("render: frame too large (%zu workgroups)", blocks);
       return RTG_ERR_INVALID;
@@ -768,26 +737,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   const size_t lds = frameLds + (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) +
                                             (size_t)ctx->n4 * 16)
                                          : 0);
-  if (variant % 100 == 10) {
-    if (!ctx->queue) {
-      HIP_TRY(hipMalloc(&ctx->queue, rtg_context::kQueueSlots * sizeof(unsigned)));
-    }
-    if (ctx->occFn != fn || ctx->occLds != lds) {
-      int perCU = 0, dev = ctx->device;
-      HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void*)fn, kBlock, lds));
-      hipDeviceProp_t p;
-      HIP_TRY(hipGetDeviceProperties(&p, dev));
-      ctx->occFn = fn;
-      ctx->occLds = lds;
-      ctx->occBlocks = (unsigned)(perCU > 0 ? perCU : 1) * (unsigned)p.multiProcessorCount;
-    }
-    const unsigned tiles = ((width + 7u) / 8u) * ((rows + 7u) / 8u);
-    const unsigned need = (tiles + 3u) / 4u;  // 4 waves per workgroup
-    a.queue = ctx->queue + (ctx->queueNext++ % rtg_context::kQueueSlots);
-    HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(unsigned), (hipStream_t)stream));
-    grid = dim3(need < ctx->occBlocks ? need : ctx->occBlocks, 1);
-  }
-  if (variant == 13) {
+  if (ctx->opts.flags & RTG_LAUNCH_TIMELINE) {
     const size_t waves = (size_t)grid.x * grid.y * (threads / 64);
     if (ctx->timelineCap < waves) {
       (void)hipFree(ctx->timeline);

@@ -248,8 +248,10 @@ class Context:
                                            _ptr(self._lgt), len(self._lgt)),
                "rtg_context_set_scene")
 
-    def set_variant(self, variant: int):
-        opts = (ctypes.c_int * 8)(variant, 0, 0, 0, 0, 0, 0, 0)
+    LAUNCH_TIMELINE = 1  # RTG_LAUNCH_TIMELINE
+
+    def set_variant(self, variant: int, flags: int = 0):
+        opts = (ctypes.c_int * 8)(variant, flags, 0, 0, 0, 0, 0, 0)
         _check(lib().rtg_set_launch_opts(self._h, ctypes.cast(opts, ctypes.c_void_p)),
                "rtg_set_launch_opts")
 

@@ -70,6 +70,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 4: p = rtg::shade_pixel_nodes<S, 2>(sc, cam, x, y); break;
       case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
       case 8: p = rtg::shade_pixel<S, 3, true>(sc, cam, x, y); break;
+      case 0:
       case 14: {  // sample-parallel kernel: samples traced one by one, summed in order
         p = rtg::v3(0.f, 0.f, 0.f);
         for (int s = 0; s < cam.nAA * cam.nAA; ++s) {
@@ -81,7 +82,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
         }
         break;
       }
-      default: {
+      default: {  // tile kernel (variant 9)
         // per-pixel primary cull: a stricter (smaller) bundle than the GPU's
         // per-wave one, so it exercises the cull's conservativeness harder
         uint64_t sel = ~0ull;

@@ -106,7 +106,7 @@ def test_random_scenes_vs_oracle(R, oracle):
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
 
 
-@pytest.mark.parametrize("variant", [14, 10])
+@pytest.mark.parametrize("variant", [0, 9, 14])
 def test_random_scenes_vs_oracle_variants(R, oracle, torch_cuda, variant):
     """Mapping variants over random scenes, sizes and alias factors (the
     sample-parallel kernel packs 64 // nAA^2 pixels per wave and falls back to
@@ -167,10 +167,10 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
     ctx.close()
 
 
-@pytest.mark.parametrize("variant", [10, 11, 12, 14])
-def test_queue_kernel_full_frames(R, golden, torch_cuda, variant):
-    """The work-queue kernel over whole frames, sharded frames, row lists and
-    back-to-back launches on two streams (each launch has its own counter)."""
+@pytest.mark.parametrize("variant", [0, 9, 14])
+def test_variant_full_frames(R, golden, torch_cuda, variant):
+    """Kernel mappings over whole frames, sharded frames, row lists and
+    back-to-back launches on two streams."""
     from rtg_amd import dist
     torch = torch_cuda
     ctx = R.Context(0)
@@ -247,7 +247,7 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 100, 108, 110])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 100, 108])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda
@@ -265,4 +265,27 @@ def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert bits_equal(got, want), (name, variant, first_mismatch(got, want))
+    ctx.close()
+
+
+@pytest.mark.parametrize("variant", [9, 0])
+def test_wave_timeline_diagnostic(R, golden, torch_cuda, variant):
+    """RTG_LAUNCH_TIMELINE: one record per wave, output unchanged."""
+    torch = torch_cuda
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    W, H, S = c["W"], c["H"], c["stack_size"]
+    ctx = R.Context(0)
+    ctx.set_scene(sph, lg)
+    ctx.set_variant(variant, ctx.LAUNCH_TIMELINE)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    ctx.render_device(W, H, out.data_ptr(), stack_size=S,
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert canon_md5(out.cpu().numpy()) == c["fb_md5"]
+    rec = ctx.diag_timeline()
+    waves = ((W + 15) // 16) * ((H + 15) // 16) * 4 if variant == 9 else -(-(W * H) // 7)
+    assert len(rec) == waves
+    dur = (rec[:, 1].astype(np.int64) - rec[:, 0].astype(np.int64)) % (1 << 32)
+    assert (dur < 100_000_000).all()  # < 1 s each
     ctx.close()

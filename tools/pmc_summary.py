@@ -28,7 +28,7 @@ def source_md5():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="trace_kernel")
+    ap.add_argument("--kernel", default="rtg::trace_", help="kernel-name substring")
     ap.add_argument("--json", default=None)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--variant", type=int, default=0)

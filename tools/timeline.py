@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Wave-occupancy timeline of the trace kernel (diagnostic, GPU box).
 
-Renders a config with the timeline variant (13 = the default kernel plus one
+Renders a config with a kernel variant and the RTG_LAUNCH_TIMELINE flag (one
 {start, end, HW_ID, XCC_ID} record per wave, s_memrealtime at 100 MHz) and
 reports how full the SIMDs' wave slots were over the launch: mean resident
 waves per SIMD, the occupancy curve over time, wave-duration spread, and the
@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--variant", type=int, default=13)
+    ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--waves-per-block", type=int, default=4)
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
@@ -37,7 +37,7 @@ def main():
     W, H, S = c["W"], c["H"], c["stack_size"]
     ctx = R.Context(0)
     ctx.set_scene(sph, lg)
-    ctx.set_variant(a.variant)
+    ctx.set_variant(a.variant, ctx.LAUNCH_TIMELINE)
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     for _ in range(3):
