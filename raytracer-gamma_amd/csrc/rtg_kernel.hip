@@ -117,6 +117,8 @@ struct DevScene {
     return v3(g.x, g.y, g.z);
   }
   __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
+  // |0 - c_i|^2 - r_i^2: the c term of a ray from the origin (primary rays)
+  __device__ __forceinline__ float origin_c(unsigned i) const { return crad2[n + i]; }
   __device__ __forceinline__ Mat mat(int i) const {
     const auto p = mats + 8 * i;
     Mat r;
@@ -163,7 +165,7 @@ __device__ __forceinline__ float canon_nan(float v) {
 template <int S, int kVariant>
 struct MinWaves {
   static constexpr int value =
-      ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant == 14) && S <= 6) ? 7 : 1;
+      ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
 };
 
 // Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
@@ -317,8 +319,13 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   const bool valid = pl < PPW && p < total;
   unsigned x = 0, lr = 0, gy = 0;
   if (valid) {
-    lr = (unsigned)(p / a.W);
-    x = (unsigned)(p - (size_t)lr * a.W);
+    if (total <= 0xFFFFFFFFull) {  // wave-uniform: 32-bit division
+      lr = (unsigned)p / a.W;
+      x = (unsigned)p - lr * a.W;
+    } else {
+      lr = (unsigned)(p / a.W);
+      x = (unsigned)(p - (size_t)lr * a.W);
+    }
     gy = a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
   }
   const int si = (int)(s / nAA), sj = (int)(s - (unsigned)si * nAA);
@@ -370,7 +377,7 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
 
 template <int kVariant>
 struct SampleThreads {
-  static constexpr int value = (kVariant == 14) ? kBlock : 64;
+  static constexpr int value = (kVariant == 14) ? kBlock : (kVariant == 16) ? 128 : 64;
 };
 
 // One launch, one pixel group per wave: one-wave workgroups (default), or
@@ -429,7 +436,8 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
 //   0 (default) sample-parallel: one primary sample per lane, one-wave
-//     workgroups (trace_samples_kernel); falls back to 9 when nAA > 8
+//     workgroups, scene tables read from global memory (trace_samples_kernel);
+//     falls back to 9 when nAA > 8
 //   1 per-sample recursion, one sphere per step (first kernel)
 //   2 one-query-per-iteration state machine + candidate masks
 //   3 one-query-per-iteration state machine, four spheres per step
@@ -442,12 +450,17 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 //     pixel (per-sample recursion + two-pass candidate-mask queries + per-wave
 //     primary cull), 7 waves/SIMD; the default until the sample-parallel kernel
 //   14 as 0 with four-wave workgroups
-//   (10-12, 15, 16: work-queue and workgroup-size trials, removed: DESIGN.md)
+//   15 same kernel as 0 (kept as an alias for A/B scripts)
+//   16 as 17 with two-wave workgroups
+//   17 as 0 with the materials/geometry staged in LDS per workgroup
+//   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
-  if constexpr (V == 0 || V == 14)
+  if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
+  else if constexpr (V == 0 || V == 15)
+    return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
 }
@@ -463,6 +476,9 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 8: return trace_fn_v<S, 8>(lds);
     case 9: return trace_fn_v<S, 9>(lds);
     case 14: return trace_fn_v<S, 14>(lds);
+    case 15: return trace_fn_v<S, 15>(lds);
+    case 16: return trace_fn_v<S, 16>(lds);
+    case 17: return trace_fn_v<S, 17>(lds);
     case 108: return trace_fn_v<S, 108>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
@@ -667,14 +683,18 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     rtg_set_error("render: no context/scene");
     return RTG_ERR_INVALID;
   }
-  const bool ldsMats = ctx->n + 1 <= kLdsMatMax;
+  bool ldsMats = ctx->n + 1 <= kLdsMatMax;
   KernelArgs a;
   int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
   if (rc) return rc;
   int variant = ctx->opts.variant;
   // sample-parallel kernel: needs all of a pixel's samples in one wave
   // sample-parallel kernels need all of a pixel's samples in one wave
-  if ((variant == 0 || variant == 14) && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = 9;
+  const bool sampleKernel = variant == 0 || (variant >= 14 && variant <= 17);
+  if (sampleKernel && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = 9;
+  // the default sample kernel reads materials/geometry from global memory
+  // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
+  if (variant == 0 || variant == 15) ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {
     rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
@@ -721,10 +741,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   HIP_TRY(hipSetDevice(ctx->device));
   unsigned threads = (unsigned)kBlock;
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
-  if (variant == 0 || variant == 14) {
+  if (variant == 0 || (variant >= 14 && variant <= 17)) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);
     const size_t waves = ((size_t)width * rows + ppw - 1) / ppw;
-    const unsigned tpb = variant == 0 ? 64u : (unsigned)kBlock;
+    const unsigned tpb = variant == 14 ? 256u : variant == 16 ? 128u : 64u;
     const size_t blocks = (waves + tpb / 64 - 1) / (tpb / 64);
     threads = tpb;
     if (blocks > 0x7FFFFFFFu) {

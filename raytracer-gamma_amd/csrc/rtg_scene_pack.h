@@ -6,6 +6,8 @@
 // hoisted to the host with the same float operation (-ffp-contract=off):
 //   r*r                       raytracer.h:100
 //   (radius + 1e-6f)^2        raytracer.h:259-264
+//   |0 - c|^2 - r*r           raytracer.h:99-101 for a ray from the origin
+//                              (every primary ray, main.cpp:417)
 //   camera constants          main.cpp:384-402
 #pragma once
 
@@ -20,7 +22,9 @@
 namespace rtg {
 
 // Device image of a scene.  geom: n x {x, y, z, r*r} followed by NaN padding
-// records up to n4 + 4 (n4 = n rounded up to 4); crad2: n x (r+1e-6)^2;
+// records up to n4 + 4 (n4 = n rounded up to 4); crad2: n x (r+1e-6)^2, then
+// n x the primary-ray c term |0 - c|^2 - r^2 (same float operations and order
+// as the query's vdot(disp, disp) - r2 with disp = 0 - c, exact negation);
 // mats: (n+1) x {matte.xyz, gloss.xyz, opacity, n} with [n] = background
 // {0,0,0, 0,0,0, 0, 1.0} (raytracer.h:694-697; opacity 0);
 // lights: m x {pos.xyz, col.xyz}.  Arrays are never empty (padded to 1).
@@ -37,7 +41,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   ps->n4 = (n + 3u) & ~3u;
   // Padding records are NaN spheres: their radicand is NaN, never >= 0.
   ps->geom.assign((size_t)(ps->n4 + 4) * 4, __builtin_nanf(""));
-  ps->crad2.assign(n ? n : 1, 0.f);
+  ps->crad2.assign(n ? 2 * (size_t)n : 1, 0.f);
   ps->mats.assign((size_t)(n + 1) * 8, 0.f);
   ps->lights.assign((size_t)(m ? m : 1) * 6, 0.f);
   for (unsigned i = 0; i < n; ++i) {
@@ -47,6 +51,8 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     g[3] = s.radius * s.radius;
     const float rc = s.radius + 1.0e-6f;
     ps->crad2[i] = rc * rc;
+    const float dx = 0.f - s.pos.x, dy = 0.f - s.pos.y, dz = 0.f - s.pos.z;
+    ps->crad2[n + i] = (((dx * dx) + (dy * dy)) + (dz * dz)) - g[3];
     float* mt = &ps->mats[(size_t)i * 8];
     mt[0] = s.material.matteColour.x; mt[1] = s.material.matteColour.y;
     mt[2] = s.material.matteColour.z; mt[3] = s.material.glossColour.x;

@@ -34,6 +34,8 @@
 // f32 division and sqrt are the HIP defaults and are checked by the GPU tests).
 #pragma once
 
+#include <string.h>
+
 #include <stdint.h>
 #include <math.h>
 
@@ -497,34 +499,41 @@ RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
 // together instead of every sphere's branch running for whichever lanes need
 // it.  The radicand is recomputed with the same operations, so it is the same
 // value.  Spheres are processed in chunks of 32 (one mask word).
+// Shift the sign bit of v into acc from the right: acc = acc << 1 | sign(v)
+// (one v_alignbit_b32).  rad >= 0 <=> sign clear for every radicand the query
+// can produce except NaN (b*b is never -0, so rad is never -0); a NaN with
+// the sign clear becomes a candidate, which pass 2 then rejects.
+RTG_HD unsigned push_sign(unsigned acc, float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(acc, __float_as_uint(v), 31);
+#else
+  unsigned u;
+  memcpy(&u, &v, 4);
+  return (acc << 1) | (u >> 31);
+#endif
+}
+
 template <class Scene>
 RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, V3 o, V3 d,
                                float a4) {
-  unsigned mask = 0;
-  unsigned k = 0;
-  for (; k + 4 <= cnt; k += 4) {
+  // Groups of 4 from the last to the first, so sphere base + k lands in bit k;
+  // records past n are NaN padding (PackedScene), masked off below.
+  unsigned neg = 0;
+  for (int k = (int)((cnt + 3u) & ~3u) - 4; k >= 0; k -= 4) {
     V3 c[4];
     float r2[4];
-    sc.sphere4(base + k, c, r2);
+    sc.sphere4(base + (unsigned)k, c, r2);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 3; q >= 0; --q) {
       const V3 disp = vsub(o, c[q]);
       const float b = 2.0f * vdot(d, disp);
       const float cc = vdot(disp, disp) - r2[q];
       const float rad = (b * b) - (a4 * cc);
-      mask |= (rad >= 0.0f) ? (1u << (k + q)) : 0u;
+      neg = push_sign(neg, rad);
     }
   }
-  for (; k < cnt; ++k) {
-    float r2;
-    const V3 c = sc.sphere(base + k, r2);
-    const V3 disp = vsub(o, c);
-    const float b = 2.0f * vdot(d, disp);
-    const float cc = vdot(disp, disp) - r2;
-    const float rad = (b * b) - (a4 * cc);
-    mask |= (rad >= 0.0f) ? (1u << k) : 0u;
-  }
-  return mask;
+  const unsigned all = cnt >= 32u ? ~0u : ((1u << cnt) - 1u);
+  return ~neg & all;
 }
 
 RTG_HD int lowest_bit(unsigned m) {
@@ -591,14 +600,16 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
   float minT = 1000.f;
   int best = -1;
   uint64_t cand = 0;
+  // The primary ray starts at the origin (main.cpp:417): disp = 0 - c = -c
+  // exactly, so b = 2 d.disp = -(2 d.c) and b*b is (2 d.c)^2; the c term
+  // |disp|^2 - r^2 is precomputed per sphere (origin_c).  Same radicand bits.
+  (void)o;
   for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform: scalar loop + scalar loads
     const unsigned i = (unsigned)__builtin_ctzll(m);
     float r2;
     const V3 c = sc.sphere(i, r2);
-    const V3 disp = vsub(o, c);
-    const float b = 2.0f * vdot(d, disp);
-    const float cc = vdot(disp, disp) - r2;
-    const float rad = (b * b) - (q.a4 * cc);
+    const float b = 2.0f * vdot(d, c);
+    const float rad = (b * b) - (q.a4 * sc.origin_c(i));
     cand |= (rad >= 0.0f) ? (1ull << i) : 0ull;
   }
   while (cand) {
@@ -616,36 +627,51 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
 
 // Conservative cull of spheres for a bundle of primary rays (origin 0,
 // main.cpp:417): every ray direction is (X, Y, zoom) with X in [x0, x1],
-// Y in [y0, y1] (main.cpp:432-436, before normalisation).  Returns bit i set
-// unless sphere i provably has no forward intersection with any such ray:
-// its angular distance from the bundle's axis exceeds the bundle's half-angle
-// plus the sphere's angular radius by a 1e-3 rad margin (radius also inflated
-// by 1e-3 relative + 1e-3 absolute), far above the float error of either the
-// bounds or the reference's own root test.  Only spheres 0..63 can be culled
-// (bits are kept for all when n > 64 is handled by the caller).
+// Y in [y0, y1] (main.cpp:432-436, before normalisation).  Returns false only
+// if sphere c, r provably has no forward intersection with any such ray: the
+// angle between the bundle's axis U and c exceeds the bundle's half-angle
+// theta plus the sphere's angular radius alpha, compared through cosines,
+// cos(angle) < cos(theta + alpha) - 2e-3 with
+// cos(theta + alpha) = cos(theta) cos(alpha) - sin(theta) sin(alpha)
+// (cos is 1-Lipschitz, so 2e-3 covers an angle margin of 2e-3 rad), and the
+// radius inflated by 1e-3 relative + 1e-3 absolute.  Those margins are far
+// above the float error of the bounds, of the hardware reciprocal square
+// roots used here (about 1 ulp) and of the reference's own root test.
+// Bundles wider than 60 degrees, and spheres at or around the origin, are
+// never culled.
+RTG_HD float cull_rsq(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rsqf(x);
+#else
+  return 1.0f / sqrtf(x);
+#endif
+}
+
 RTG_HD bool primary_sphere_possible(V3 c, float r, float x0, float x1, float y0, float y1,
                                     float zoom) {
   if (!(zoom != 0.f)) return true;
   const float xc = 0.5f * (x0 + x1), yc = 0.5f * (y0 + y1);
-  const float la = sqrtf(xc * xc + yc * yc + zoom * zoom);
-  const V3 U = v3(xc / la, yc / la, zoom / la);
-  float cosTheta = 1.f;
+  const float ila = cull_rsq(xc * xc + yc * yc + zoom * zoom);
+  const V3 U = v3(xc * ila, yc * ila, zoom * ila);
+  float cosT = 1.f;
   const float xs[2] = {x0, x1}, ys[2] = {y0, y1};
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
-      const float lc = sqrtf(xs[a] * xs[a] + ys[b] * ys[b] + zoom * zoom);
-      const float cs = (U.x * xs[a] + U.y * ys[b] + U.z * zoom) / lc;
-      cosTheta = fminf(cosTheta, cs);
+      const float il = cull_rsq(xs[a] * xs[a] + ys[b] * ys[b] + zoom * zoom);
+      cosT = fminf(cosT, (U.x * xs[a] + U.y * ys[b] + U.z * zoom) * il);
     }
-  const float theta = acosf(fmaxf(-1.f, fminf(1.f, cosTheta)));
-  const float L = sqrtf(vdot(c, c));
+  if (!(cosT >= 0.5f)) return true;  // wide (or NaN) bundle
+  const float L2 = vdot(c, c);
+  const float iL = cull_rsq(L2);
   const float rr = r * 1.001f + 1.0e-3f;
-  if (!(L > rr * 1.001f)) return true;  // origin inside or near the sphere (or NaN)
-  const float alpha = asinf(fminf(1.f, rr / L));
-  const float lim = theta + alpha + 1.0e-3f;
-  if (!(lim < 3.1f)) return true;
-  const float cosPhi = vdot(U, c) / L;
-  return cosPhi >= cosf(lim);
+  const float sa = rr * iL;  // sin(alpha)
+  if (!(sa < 0.999f)) return true;  // origin inside or near the sphere (or NaN)
+  const float ca2 = 1.f - sa * sa, st2 = fmaxf(0.f, 1.f - cosT * cosT);
+  const float ca = ca2 * cull_rsq(ca2);
+  const float st = st2 > 0.f ? st2 * cull_rsq(st2) : 0.f;
+  const float cosLim = cosT * ca - st * sa;  // theta + alpha < 60 + 90 degrees
+  const float cosPhi = vdot(U, c) * iL;
+  return cosPhi >= cosLim - 2.0e-3f;
 }
 
 // Two-pass query for scenes of at most 64 spheres (the common case), tuned:

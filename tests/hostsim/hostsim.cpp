@@ -40,6 +40,7 @@ struct HostScene {
     for (int k = 0; k < 4; ++k) c[k] = sphere(i + k, r2[k]);
   }
   float contain_r2(unsigned i) const { return crad2[i]; }
+  float origin_c(unsigned i) const { return crad2[n + i]; }
   rtg::Mat mat(int i) const {
     const float* p = mats + 8 * i;
     rtg::Mat r;
@@ -130,4 +131,49 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
     }
   }
   return 0;
+}
+
+// Conservativeness of the primary-ray cull (primary_sphere_possible): over
+// every group of `group` consecutive pixels of a W x H frame (the sample
+// kernel's wave), bound the group's sample directions as the kernel does,
+// then count spheres the cull drops although one of those samples hits them
+// (exact ray_sphere from the origin).  *culled counts the drops in total.
+extern "C" long hostsim_cull_violations(const rtg_sphere* spheres, unsigned n, unsigned W,
+                                        unsigned H, float zoom, float aa, unsigned group,
+                                        long* culled) {
+  rtg::PackedScene ps;
+  rtg::pack_scene(spheres, n, nullptr, 0, &ps);
+  rtg::Camera cam;
+  if (rtg::make_camera(W, H, zoom, aa, &cam)) return -1;
+  HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, 0, ps.n4};
+  long bad = 0, drop = 0;
+  const size_t total = (size_t)W * H;
+  for (size_t p0 = 0; p0 < total; p0 += group) {
+    float x0 = 3e38f, x1 = -3e38f, y0 = 3e38f, y1 = -3e38f;
+    for (size_t p = p0; p < p0 + group && p < total; ++p)
+      for (int i = 0; i < cam.nAA; ++i)
+        for (int j = 0; j < cam.nAA; ++j) {
+          float rx, ry;
+          rtg::sample_dir(cam, (unsigned)(p % W), (unsigned)(p / W), i, j, rx, ry);
+          x0 = fminf(x0, rx); x1 = fmaxf(x1, rx); y0 = fminf(y0, ry); y1 = fmaxf(y1, ry);
+        }
+    for (unsigned k = 0; k < n; ++k) {
+      float r2;
+      const rtg::V3 c = sc.sphere(k, r2);
+      if (rtg::primary_sphere_possible(c, sqrtf(r2), x0, x1, y0, y1, cam.zoom)) continue;
+      ++drop;
+      for (size_t p = p0; p < p0 + group && p < total; ++p)
+        for (int i = 0; i < cam.nAA; ++i)
+          for (int j = 0; j < cam.nAA; ++j) {
+            float rx, ry;
+            const rtg::V3 d = rtg::sample_dir(cam, (unsigned)(p % W), (unsigned)(p / W), i, j, rx, ry);
+            const rtg::RayQ q = rtg::make_query(rtg::v3(0.f, 0.f, 0.f), d);
+            bool res;
+            rtg::ray_sphere(q, c, r2, res);
+            if (res) ++bad;
+          }
+    }
+  }
+  if (culled) *culled = drop;
+  return bad;
 }

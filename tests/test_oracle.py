@@ -191,3 +191,41 @@ def test_kernel_traversal_c1_full_frame(hostsim, variant, golden):
     sph, lg = load_scene("c1", c["spheres"], c["lights"])
     got = _hostsim_render(hostsim, sph, lg, c["W"], c["H"], c["stack_size"])
     assert canon_md5(got) == c["fb_md5"]
+
+
+@pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
+def test_primary_cull_is_conservative(hostsim, golden, name):
+    """primary_sphere_possible never drops a sphere that a sample of the
+    bundle hits (exact root test), over whole small frames of every config,
+    for the sample kernel's 7-pixel groups and the tile kernel's rows."""
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
+    f = hostsim.hostsim_cull_violations
+    f.restype = ctypes.c_long
+    for W, H, group in [(96, 54, 7), (160, 90, 8), (64, 48, 1)]:
+        culled = ctypes.c_long(0)
+        bad = f(P(sph), len(sph), W, H, ctypes.c_float(-4.0), ctypes.c_float(3.0), group,
+                ctypes.byref(culled))
+        assert bad == 0, (name, W, H, group, bad)
+        if len(sph) > 3:
+            assert culled.value > 0  # the cull does drop spheres
+
+
+def test_primary_cull_random_scenes(hostsim):
+    rng = np.random.default_rng(4242)
+    f = hostsim.hostsim_cull_violations
+    f.restype = ctypes.c_long
+    total_culled = 0
+    for trial in range(30):
+        n = int(rng.integers(1, 40))
+        sph, _ = random_scene(rng, n, 0)
+        zoom = float(rng.choice([-4.0, -2.0, -7.0, 3.0, 0.5]))
+        if zoom > 0:
+            sph["pos"][:, 2] *= -1.0
+        aa = float(rng.choice([1.0, 2.0, 3.0, 4.0]))
+        culled = ctypes.c_long(0)
+        bad = f(P(sph), n, 48, 36, ctypes.c_float(zoom), ctypes.c_float(aa), 7,
+                ctypes.byref(culled))
+        assert bad == 0, (trial, n, zoom, aa, bad)
+        total_culled += culled.value
+    assert total_culled > 0
