@@ -117,6 +117,7 @@ struct Frame {
 struct RayQ {
   V3 o, d;
   float a4, den, y;
+  float ap, app;  // pass-1 screen: a (1 - K) and 2 K a, K = 2^-16 (pass1_rad)
   bool fast;
 };
 
@@ -127,6 +128,8 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   const float a = vdot(d, d);
   q.a4 = 4.0f * a;
   q.den = 2.0f * a;
+  q.ap = a * (1.0f - 0x1p-16f);
+  q.app = a * 0x1p-15f;
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
   q.y = 1.0f / q.den;
   return q;
@@ -513,9 +516,29 @@ RTG_HD unsigned push_sign(unsigned acc, float v) {
 #endif
 }
 
+// Pass-1 screen for one sphere: a value whose sign bit is clear whenever the
+// reference's radicand test (raytracer.h:99-108, ray_sphere above) accepts.
+// With p = o - c (the same float subtraction as the reference), x = d.p and
+// cc = |p|^2 - r^2 evaluated with fused multiply-adds, it returns
+//   x^2 - a cc (1 - K) + 2 K a r^2 + 2^-100  =  x^2 - a cc + K a (|p|^2 + r^2) + tiny,
+// i.e. the true radicand / 4 plus a slack of K = 2^-16 relative to its terms'
+// magnitude a (|p|^2 + r^2).  Both this and the reference's own evaluation
+// are within ~40 ulps of those magnitudes of the exact value, so the slack
+// (2^8 ulps) covers both: a sphere the reference accepts always passes; the
+// few near-tangent extras are rejected by pass 2's exact test.  The 2^-100
+// floor keeps the screen open where the terms underflow.  13 VALU ops per
+// sphere instead of 19; tests/test_oracle.py checks the superset property
+// on adversarial near-tangent cases.
+RTG_HD float pass1_rad(const RayQ& q, V3 c, float r2) {
+  const V3 p = vsub(q.o, c);
+  const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+  const float cc = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -r2)));
+  const float t = fmaf(q.app, r2, 0x1p-100f);
+  return fmaf(x, x, fmaf(-q.ap, cc, t));
+}
+
 template <class Scene>
-RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, V3 o, V3 d,
-                               float a4) {
+RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, const RayQ& q) {
   // Groups of 4 from the last to the first, so sphere base + k lands in bit k;
   // records past n are NaN padding (PackedScene), masked off below.
   unsigned neg = 0;
@@ -524,13 +547,7 @@ RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, V3 
     float r2[4];
     sc.sphere4(base + (unsigned)k, c, r2);
 #pragma unroll
-    for (int q = 3; q >= 0; --q) {
-      const V3 disp = vsub(o, c[q]);
-      const float b = 2.0f * vdot(d, disp);
-      const float cc = vdot(disp, disp) - r2[q];
-      const float rad = (b * b) - (a4 * cc);
-      neg = push_sign(neg, rad);
-    }
+    for (int j = 3; j >= 0; --j) neg = push_sign(neg, pass1_rad(q, c[j], r2[j]));
   }
   const unsigned all = cnt >= 32u ? ~0u : ((1u << cnt) - 1u);
   return ~neg & all;
@@ -552,7 +569,7 @@ RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
   const unsigned n = sc.n;
   for (unsigned base = 0; base < n; base += 32) {
     const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;
-    unsigned mask = candidate_mask(sc, base, cnt, o, d, q.a4);
+    unsigned mask = candidate_mask(sc, base, cnt, q);
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
@@ -574,7 +591,7 @@ RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
   const unsigned n = sc.n;
   for (unsigned base = 0; base < n; base += 32) {
     const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;
-    unsigned mask = candidate_mask(sc, base, cnt, o, d, q.a4);
+    unsigned mask = candidate_mask(sc, base, cnt, q);
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;

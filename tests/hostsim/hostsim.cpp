@@ -4,6 +4,9 @@
 // kernel's restructured algorithm (frame stack, stale-register handling,
 // leaf doubling, early-exit shadow rays) bit for bit against the oracle
 // without a GPU.  It is not part of librtg.so and no product path calls it.
+#include <math.h>
+#include <string.h>
+
 #include <vector>
 
 #include "rtg.h"
@@ -175,5 +178,66 @@ extern "C" long hostsim_cull_violations(const rtg_sphere* spheres, unsigned n, u
     }
   }
   if (culled) *culled = drop;
+  return bad;
+}
+
+// Pass-1 screen (pass1_rad) vs the reference's radicand test on adversarial
+// ray/sphere pairs: random origins, directions (unnormalised too) and scales,
+// with the radius set so the ray passes within a relative 1e-7..1e-3 of
+// tangency, and origins on the sphere surface (secondary rays).  Returns the
+// number of pairs the reference accepts but the screen drops; *accepted and
+// *extra count reference accepts and screen-only accepts.
+extern "C" long hostsim_pass1_check(long trials, unsigned long long seed, long* accepted,
+                                    long* extra) {
+  unsigned long long st = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto u01 = [&]() {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  };
+  long bad = 0, acc = 0, ext = 0;
+  for (long t = 0; t < trials; ++t) {
+    const double scale = pow(10.0, -3.0 + 6.0 * u01());
+    rtg::V3 c = rtg::v3((float)((u01() - 0.5) * 20 * scale), (float)((u01() - 0.5) * 20 * scale),
+                        (float)((u01() - 0.5) * 20 * scale));
+    double dx = u01() - 0.5, dy = u01() - 0.5, dz = u01() - 0.5;
+    const double dl = sqrt(dx * dx + dy * dy + dz * dz);
+    const double dscale = (t % 3 == 0) ? 1.0 / dl : (0.1 + 3.0 * u01());
+    rtg::V3 d = rtg::v3((float)(dx * dscale), (float)(dy * dscale), (float)(dz * dscale));
+    rtg::V3 o;
+    float r;
+    const int mode = (int)(t % 4);
+    if (mode == 3) {  // origin on the sphere surface, random direction
+      r = (float)(scale * (0.1 + u01()));
+      double ux = u01() - 0.5, uy = u01() - 0.5, uz = u01() - 0.5;
+      const double ul = sqrt(ux * ux + uy * uy + uz * uz);
+      o = rtg::v3((float)(c.x + r * ux / ul), (float)(c.y + r * uy / ul), (float)(c.z + r * uz / ul));
+    } else {  // origin elsewhere, radius = distance(center, line) * (1 +- tiny)
+      o = rtg::v3((float)((u01() - 0.5) * 20 * scale), (float)((u01() - 0.5) * 20 * scale),
+                  (float)((u01() - 0.5) * 20 * scale));
+      const double px = (double)o.x - c.x, py = (double)o.y - c.y, pz = (double)o.z - c.z;
+      const double dd = (double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z;
+      const double pd = px * d.x + py * d.y + pz * d.z;
+      const double dist2 = px * px + py * py + pz * pz - pd * pd / dd;
+      const double rel = pow(10.0, -7.0 + 4.0 * u01()) * (u01() < 0.5 ? -1.0 : 1.0);
+      r = (float)(sqrt(fmax(dist2, 0.0)) * (1.0 + rel));
+    }
+    const float r2 = r * r;
+    const rtg::RayQ q = rtg::make_query(o, d);
+    // reference radicand (raytracer.h:99-108)
+    const rtg::V3 disp = rtg::vsub(o, c);
+    const float b = 2.0f * rtg::vdot(d, disp);
+    const float cc = rtg::vdot(disp, disp) - r2;
+    const float rad = (b * b) - (q.a4 * cc);
+    const bool ref = rad >= 0.0f;
+    const float s = rtg::pass1_rad(q, c, r2);
+    unsigned u;
+    memcpy(&u, &s, 4);
+    const bool scr = (u >> 31) == 0;
+    if (ref) ++acc;
+    if (ref && !scr) ++bad;
+    if (!ref && scr) ++ext;
+  }
+  if (accepted) *accepted = acc;
+  if (extra) *extra = ext;
   return bad;
 }
