@@ -1,17 +1,15 @@
-// rtg_kernel.hip — CDNA4 (gfx950) kernels and the device half of the C ABI.
+// rtg_kernel.hip — launch code and the device half of the C ABI of librtg.so.
 //
-// Replaces the OpenCL kernel `raytrace` (raytrace_kernel.cl:870-973) and its
-// host orchestration (main.cpp:277-363, 456-468), computing the reference CPU
-// path's framebuffer (raytracer.h) bit for bit; see rtg_trace.h for the
-// traversal and DESIGN.md for the layout and roofline.
+// Replaces the host orchestration of the OpenCL kernel `raytrace`
+// (main.cpp:277-363, 456-468): scene upload into a persistent context, the
+// trace launch (kernels in rtg_trace_kernels.h, one object per stack size),
+// and the PPM helpers on the device (max colour, byte conversion).
 //
-// Launch geometry: one work-item per pixel; a 256-thread workgroup covers a
-// 16x16 pixel tile and each 64-lane wave an 8x8 sub-tile, so the rays of a
-// wave are spatially coherent and take similar paths through the Whitted tree.
-// The sphere loop index is wave-uniform, so sphere records are read with
-// scalar loads into SGPRs (no VGPRs, no LDS traffic); per-lane material
-// lookups (the hit sphere / refractive medium) come from an LDS copy of the
-// material table staged once per workgroup.
+// Launch geometry of the default (sample-parallel) kernel: one-wave
+// workgroups, each wave floor(64 / nAA^2) consecutive pixels of the shard
+// with one primary sample per lane (7 pixels x 9 samples at nAA = 3); the
+// sphere loop index is wave-uniform, so sphere records are read with scalar
+// loads into SGPRs.  See DESIGN.md §4.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -24,7 +22,7 @@
 
 #include "rtg.h"
 #include "rtg_internal.h"
-#include "rtg_trace.h"
+#include "rtg_trace_kernels.h"
 #include "rtg_scene_pack.h"
 
 #define HIP_TRY(expr)                                                              \
@@ -38,362 +36,6 @@
   } while (0)
 
 namespace rtg {
-
-constexpr int kBlock = 256;
-// Materials staged in LDS when the table fits (n+1 records of 32 B).
-constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
-
-// Device scene: geometry SoA-ish float4 {x, y, z, r*r}, (r + 1e-6f)^2, the
-// material table (n+1 x 8 floats; [n] = background), lights (m x 6 floats).
-// Read-only scene arrays are accessed through the constant address space
-// (addrspace 4): with a wave-uniform index the loads become s_load into SGPRs.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define RTG_CONST __attribute__((address_space(4)))
-#else
-#define RTG_CONST
-#endif
-typedef const RTG_CONST float* cfloat_p;
-
-// Per-lane frame colours in LDS: level lv of thread t at lfr[lv * kBlock + t]
-// (16-byte records, so a wave's ds_read_b128 covers 1 KiB contiguously and is
-// bank-conflict free).
-template <int kThreads>
-struct LdsFrames {
-  FrameC* base;  // already offset by threadIdx.x
-  __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kThreads]; }
-};
-
-template <class MatPtr, bool kDiag = false, int kThreads = kBlock>
-struct DevScene {
-  FrameC* lfr;
-  __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
-  __device__ __forceinline__ LdsFrames<kThreads> frames() const {
-    return LdsFrames<kThreads>{lfr};
-  }
-  // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
-  // probe slot, summed per wave and added to KernelArgs::diag at exit.
-  mutable unsigned long long acc[kProbeSlots];
-  mutable unsigned long long t0[kProbeSlots];
-  __device__ __forceinline__ void probe_begin(int slot) const {
-    if constexpr (kDiag) {
-      __builtin_amdgcn_sched_barrier(0);
-      t0[slot] = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  __device__ __forceinline__ void probe_end(int slot) const {
-    if constexpr (kDiag) {
-      __builtin_amdgcn_sched_barrier(0);
-      acc[slot] += __builtin_amdgcn_s_memtime() - t0[slot];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  cfloat_p geom;      // n x {x, y, z, r*r}
-  cfloat_p crad2;
-  MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)
-  const float4* lgeom;  // LDS copy of geom (or the global array when it does not fit)
-  cfloat_p lights;
-  unsigned n, m;
-  unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
-
-  __device__ __forceinline__ V3 sphere(unsigned i, float& r2) const {
-    cfloat_p g = geom + 4 * i;
-    r2 = g[3];
-    return v3(g[0], g[1], g[2]);
-  }
-  // Four consecutive sphere records: one 64-byte scalar load.
-  __device__ __forceinline__ void sphere4(unsigned i, V3* c, float* r2) const {
-    cfloat_p g = geom + 4 * i;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
-      r2[k] = g[4 * k + 3];
-    }
-  }
-  // Per-lane sphere record (divergent index): from the LDS copy.
-  __device__ __forceinline__ V3 sphere_lane(unsigned i, float& r2) const {
-    const float4 g = lgeom[i];
-    r2 = g.w;
-    return v3(g.x, g.y, g.z);
-  }
-  __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
-  // |0 - c_i|^2 - r_i^2: the c term of a ray from the origin (primary rays)
-  __device__ __forceinline__ float origin_c(unsigned i) const { return crad2[n + i]; }
-  __device__ __forceinline__ Mat mat(int i) const {
-    const auto p = mats + 8 * i;
-    Mat r;
-    r.matte = v3(p[0], p[1], p[2]);
-    r.gloss = v3(p[3], p[4], p[5]);
-    r.opacity = p[6];
-    r.refr = p[7];
-    return r;
-  }
-  __device__ __forceinline__ float refr(int i) const { return mats[8 * i + 7]; }
-  __device__ __forceinline__ void light(unsigned l, V3& pos, V3& col) const {
-    cfloat_p p = lights + 6 * l;
-    pos = v3(p[0], p[1], p[2]);
-    col = v3(p[3], p[4], p[5]);
-  }
-};
-
-struct KernelArgs;
-typedef void (*TraceFn)(const KernelArgs);
-
-struct KernelArgs {
-  const float4* geom;
-  const float* crad2;
-  const float* mats;
-  const float* lights;
-  unsigned n, m, n4;
-  Camera cam;
-  unsigned W, rowsLocal, rowBlock, shard, nShards;
-  const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
-  float* dst;
-  unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
-  uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
-};
-
-__device__ __forceinline__ float canon_nan(float v) {
-  // x86 default NaN, what the reference CPU path writes (see rtg.h).
-  return (v != v) ? __uint_as_float(0xFFC00000u) : v;
-}
-
-// Minimum waves per SIMD requested from the register allocator: 7 (<= 72
-// VGPRs) where the LDS image of S-1 frame levels still admits 7 waves per
-// SIMD (S <= 6 with a small scene); measured +1-2 % over the unconstrained
-// 78-VGPR build at 6 waves/SIMD (C3, tile kernel).
-template <int S, int kVariant>
-struct MinWaves {
-  static constexpr int value =
-      ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
-};
-
-// Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
-template <int S, bool kLds, int kThreads, class Sc>
-__device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
-  extern __shared__ float4 lds4[];
-  constexpr int NF = (S > 1) ? (S - 1) : 1;
-  sc.lfr = reinterpret_cast<FrameC*>(lds4) + threadIdx.x;
-  float4* sceneLds = lds4 + NF * kThreads;
-  if constexpr (kLds) {
-    float* lmats = reinterpret_cast<float*>(sceneLds);
-    const unsigned nm = (a.n + 1) * 8;
-    for (unsigned i = threadIdx.x; i < nm; i += kThreads) lmats[i] = a.mats[i];
-    float4* lg = sceneLds + (a.n + 1) * 2;
-    for (unsigned i = threadIdx.x; i < a.n4; i += kThreads)
-      lg[i] = reinterpret_cast<const float4*>(a.geom)[i];
-    __syncthreads();
-    sc.mats = lmats;
-    sc.lgeom = lg;
-  } else {
-    sc.mats = (cfloat_p)a.mats;
-    sc.lgeom = reinterpret_cast<const float4*>(a.geom);
-  }
-  sc.geom = (cfloat_p)a.geom;
-  sc.crad2 = (cfloat_p)a.crad2;
-  sc.lights = (cfloat_p)a.lights;
-  sc.n = a.n;
-  sc.m = a.m;
-  sc.n4 = a.n4;
-}
-
-// One 8 x 8 pixel tile per wave: tile (tx, ty) of the shard's local rows.
-// Entered with the whole wave converged.
-template <int S, int kVariant, class Sc>
-__device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned tx,
-                                           unsigned ty) {
-  constexpr bool kDiag = kVariant >= 100;
-  constexpr int kBase = kDiag ? kVariant - 100 : kVariant;
-  const unsigned lane = threadIdx.x & 63u;
-  const unsigned x = tx * 8u + (lane & 7u);
-  const unsigned lr = ty * 8u + (lane >> 3);
-  const bool valid = x < a.W && lr < a.rowsLocal;
-  const unsigned gy = !valid ? 0u
-                     : a.rowList ? a.rowList[lr]
-                                 : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
-
-  // Primary-ray sphere cull for this wave (whole wave converged here): the
-  // bounds of every sample direction of the wave's pixels, then one sphere
-  // per lane against that bundle, then a ballot (see primary_sphere_possible).
-  uint64_t primSel = ~0ull;
-  bool usePrim = false;
-  if constexpr (kBase == 0 || kBase == 8 || kBase == 9) {
-    if (a.n <= 64) {
-      float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
-      if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
-      for (int off = 32; off > 0; off >>= 1) {
-        x0 = fminf(x0, __shfl_xor(x0, off));
-        x1 = fmaxf(x1, __shfl_xor(x1, off));
-        y0 = fminf(y0, __shfl_xor(y0, off));
-        y1 = fmaxf(y1, __shfl_xor(y1, off));
-      }
-      bool possible = false;
-      if (lane < a.n) {
-        const float4 g = sc.lgeom[lane];
-        possible = primary_sphere_possible(v3(g.x, g.y, g.z), sqrtf(g.w), x0, x1, y0, y1,
-                                           a.cam.zoom);
-      }
-      primSel = __ballot(possible);
-      usePrim = true;
-    }
-  }
-  if (!valid) return;
-  V3 pix;
-  unsigned long long tk0 = 0;
-  if constexpr (kDiag) {
-    for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
-    tk0 = __builtin_amdgcn_s_memtime();
-  }
-  if constexpr (kBase == 0 || kBase == 9)
-    pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
-  else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
-  else if constexpr (kBase == 8) pix = shade_pixel<S, 3, true>(sc, a.cam, x, gy, usePrim, primSel);
-  else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
-  else if constexpr (kBase == 1) pix = shade_pixel<S, 0>(sc, a.cam, x, gy);
-  else if constexpr (kBase == 2) pix = shade_pixel_persistent<S, 2>(sc, a.cam, x, gy);
-  else if constexpr (kBase == 3) pix = shade_pixel_persistent<S, 1>(sc, a.cam, x, gy);
-  else pix = shade_pixel_nodes<S, 2>(sc, a.cam, x, gy);
-  if constexpr (kDiag) {
-    sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
-    // one wave-level add per slot (values are wave-uniform: s_memtime is scalar)
-    if ((threadIdx.x & 63u) == (unsigned)__builtin_ctzll(__ballot(1)))
-      for (int k = 0; k < kProbeSlots; ++k) atomicAdd(&a.diag[k], sc.acc[k]);
-  }
-  float* o = a.dst + ((size_t)lr * a.W + x) * 3;
-  o[0] = canon_nan(pix.x);
-  o[1] = canon_nan(pix.y);
-  o[2] = canon_nan(pix.z);
-}
-
-// Timeline record of one wave (launch flag RTG_LAUNCH_TIMELINE): start/end
-// s_memrealtime (100 MHz), HW_ID (hwreg 4) and XCC_ID (hwreg 20).  Called
-// with the wave converged.
-__device__ __forceinline__ void record_wave(const KernelArgs& a, unsigned t0, size_t w) {
-  if (a.timeline == nullptr) return;
-  const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
-  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
-  if ((threadIdx.x & 63u) == 0) a.timeline[w] = make_uint4(t0, t1, hw, xcc);
-}
-
-// Tile kernels: one 8 x 8 pixel tile per wave, all samples of a pixel in its
-// lane; a workgroup is 2 x 2 tiles.
-template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value))
-void trace_kernel(const KernelArgs a) {
-  // LDS image: per-lane frame colours ((S-1) x threads x 16 B), then, when
-  // kLds, the material table (n+1) x 8 floats and the geometry n x float4.
-  constexpr int kThreads = kBlock;
-  constexpr unsigned TW = 2u, TH = 2u;
-  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100), kThreads> sc;
-  stage_scene<S, kLds, kThreads>(a, sc);
-  const unsigned wave = threadIdx.x >> 6;
-  const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
-  trace_tile<S, kVariant>(a, sc, blockIdx.x * TW + (wave % TW), blockIdx.y * TH + (wave / TW));
-  record_wave(a, t0, ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + wave);
-}
-
-// Sample-parallel form (variant 14): each lane traces ONE primary sample, so
-// a wave takes floor(64 / nAA^2) consecutive pixels (7 at 3 x 3) with their
-// samples in lane order, instead of 64 pixels x all their samples.  A heavy
-// region (deep refraction trees) is then spread over nAA^2 times as many
-// waves, which keeps the frame's last waves short (the default kernel's
-// 8 x 8 tiles of 9 samples ran up to 3 ms each on C3), and a
-// wave's primary-ray bundle is a few pixels wide, so the cull is tighter.
-// Each pixel's sum is formed in the reference's sample order
-// (main.cpp:411-452: pix += c_s * inv for s = 0 .. nAA^2-1) by its first lane
-// from the other lanes' values (ds_bpermute moves the bits unchanged).
-// Requires nAA^2 <= 64; the host launches the default kernel otherwise.
-// Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
-// rows, all their samples) traced by one wave, entered converged.
-template <int S, class Sc>
-__device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
-  const unsigned lane = threadIdx.x & 63u;
-  const unsigned nAA = (unsigned)a.cam.nAA;
-  const unsigned SP = nAA * nAA;
-  const unsigned PPW = 64u / SP;
-  const unsigned pl = lane / SP, s = lane - pl * SP;
-  const size_t p = gw * PPW + pl;
-  const size_t total = (size_t)a.W * a.rowsLocal;
-  const bool valid = pl < PPW && p < total;
-  unsigned x = 0, lr = 0, gy = 0;
-  if (valid) {
-    if (total <= 0xFFFFFFFFull) {  // wave-uniform: 32-bit division
-      lr = (unsigned)p / a.W;
-      x = (unsigned)p - lr * a.W;
-    } else {
-      lr = (unsigned)(p / a.W);
-      x = (unsigned)(p - (size_t)lr * a.W);
-    }
-    gy = a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
-  }
-  const int si = (int)(s / nAA), sj = (int)(s - (unsigned)si * nAA);
-  float rx, ry;
-  const V3 dir = sample_dir(a.cam, x, gy, si, sj, rx, ry);
-
-  // Primary-ray cull over the wave's sample directions (wave converged).
-  uint64_t primSel = ~0ull;
-  bool usePrim = false;
-  if (a.n <= 64) {
-    float x0 = valid ? rx : 3.0e38f, x1 = valid ? rx : -3.0e38f;
-    float y0 = valid ? ry : 3.0e38f, y1 = valid ? ry : -3.0e38f;
-    for (int off = 32; off > 0; off >>= 1) {
-      x0 = fminf(x0, __shfl_xor(x0, off));
-      x1 = fmaxf(x1, __shfl_xor(x1, off));
-      y0 = fminf(y0, __shfl_xor(y0, off));
-      y1 = fmaxf(y1, __shfl_xor(y1, off));
-    }
-    bool possible = false;
-    if (lane < a.n) {
-      const float4 g = sc.lgeom[lane];
-      possible = primary_sphere_possible(v3(g.x, g.y, g.z), sqrtf(g.w), x0, x1, y0, y1,
-                                         a.cam.zoom);
-    }
-    primSel = __ballot(possible);
-    usePrim = true;
-  }
-  V3 c = v3(0.f, 0.f, 0.f);
-  if (valid) {
-    c = trace_sample<S, 2>(sc, dir, sc.frames(), usePrim, primSel);
-    c = vsmul(a.cam.inv, c);
-  }
-  // Ordered per-pixel sum (whole wave converged again).
-  const unsigned base = pl * SP;
-  V3 pix = v3(0.f, 0.f, 0.f);
-  for (unsigned k = 0; k < SP; ++k) {
-    const int src = (int)((base + k) & 63u);
-    pix.x = pix.x + __shfl(c.x, src);
-    pix.y = pix.y + __shfl(c.y, src);
-    pix.z = pix.z + __shfl(c.z, src);
-  }
-  if (valid && s == 0) {
-    float* o = a.dst + ((size_t)lr * a.W + x) * 3;
-    o[0] = canon_nan(pix.x);
-    o[1] = canon_nan(pix.y);
-    o[2] = canon_nan(pix.z);
-  }
-}
-
-template <int kVariant>
-struct SampleThreads {
-  static constexpr int value = (kVariant == 14) ? kBlock : (kVariant == 16) ? 128 : 64;
-};
-
-// One launch, one pixel group per wave: one-wave workgroups (default), or
-// four-wave ones (variant 14).
-template <int S, bool kLds, int kVariant>
-__global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
-void trace_samples_kernel(const KernelArgs a) {
-  constexpr int kThreads = SampleThreads<kVariant>::value;
-  typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, false, kThreads> sc;
-  const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
-  stage_scene<S, kLds, kThreads>(a, sc);
-  const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  trace_group<S>(a, sc, gw);
-  record_wave(a, t0, gw);
-}
 
 // algebra.h:68-91 on the device: values are compared as floats (NaN never
 // wins), the running max starts at +0 so only positive values can win, and a
@@ -434,61 +76,9 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
     out[i] = ppm_byte(c[i], m);
 }
 
-// Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
-//   0 (default) sample-parallel: one primary sample per lane, one-wave
-//     workgroups, scene tables read from global memory (trace_samples_kernel);
-//     falls back to 9 when nAA > 8
-//   1 per-sample recursion, one sphere per step (first kernel)
-//   2 one-query-per-iteration state machine + candidate masks
-//   3 one-query-per-iteration state machine, four spheres per step
-//   4 node-persistent: samples chained in one node loop + candidate masks
-//   5 as 9 but frame colours in private memory instead of LDS
-//   6 as 9 without the per-wave primary-ray sphere cull
-//   (7, a converged loop with per-query bundle culls, was removed: DESIGN.md)
-//   8 as 9 with the tuned two-pass query (prefetched groups, uniform quotient path)
-//   9 tile kernel: an 8 x 8 pixel tile per wave, each lane all samples of its
-//     pixel (per-sample recursion + two-pass candidate-mask queries + per-wave
-//     primary cull), 7 waves/SIMD; the default until the sample-parallel kernel
-//   14 as 0 with four-wave workgroups
-//   15 same kernel as 0 (kept as an alias for A/B scripts)
-//   16 as 17 with two-wave workgroups
-//   17 as 0 with the materials/geometry staged in LDS per workgroup
-//   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
-//   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9
-template <int S, int V>
-static TraceFn trace_fn_v(bool lds) {
-  if constexpr (V == 14 || V == 16 || V == 17)
-    return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15)
-    return trace_samples_kernel<S, false, V>;
-  else
-    return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
-}
-template <int S>
-static TraceFn trace_fn(bool lds, int variant) {
-  switch (variant) {
-    case 100: return trace_fn_v<S, 100>(lds);
-    case 104: return trace_fn_v<S, 104>(lds);
-    case 1: return trace_fn_v<S, 1>(lds);
-    case 4: return trace_fn_v<S, 4>(lds);
-    case 5: return trace_fn_v<S, 5>(lds);
-    case 6: return trace_fn_v<S, 6>(lds);
-    case 8: return trace_fn_v<S, 8>(lds);
-    case 9: return trace_fn_v<S, 9>(lds);
-    case 14: return trace_fn_v<S, 14>(lds);
-    case 15: return trace_fn_v<S, 15>(lds);
-    case 16: return trace_fn_v<S, 16>(lds);
-    case 17: return trace_fn_v<S, 17>(lds);
-    case 108: return trace_fn_v<S, 108>(lds);
-    case 2: return trace_fn_v<S, 2>(lds);
-    case 3: return trace_fn_v<S, 3>(lds);
-    default: return trace_fn_v<S, 0>(lds);
-  }
-}
-
 static TraceFn pick_trace(int S, bool lds, int variant) {
   switch (S) {
-#define RTG_CASE(k) case k: return trace_fn<k>(lds, variant);
+#define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant);
     RTG_CASE(1) RTG_CASE(2) RTG_CASE(3) RTG_CASE(4) RTG_CASE(5) RTG_CASE(6) RTG_CASE(7)
     RTG_CASE(8) RTG_CASE(9) RTG_CASE(10) RTG_CASE(11) RTG_CASE(12) RTG_CASE(13)
     RTG_CASE(14) RTG_CASE(15) RTG_CASE(16)

@@ -1,5 +1,5 @@
 // rtg_trace.h — per-pixel Whitted traversal of raytracer-gamma, written for
-// the CDNA4 kernel in rtg_kernel.hip.
+// the CDNA4 kernels in rtg_trace_kernels.h.
 //
 // It computes exactly what the reference CPU path computes (raytracer.h +
 // raytraceStack.h + main.cpp:411-452), bit for bit, but is restructured for a
