@@ -96,6 +96,7 @@ struct rtg_context {
   float* crad2 = nullptr;
   float* mats = nullptr;
   float* lights = nullptr;
+  unsigned* smask = nullptr;  // shadow masks (null when the scene has none)
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
@@ -111,6 +112,8 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->crad2);
   (void)hipFree(c->mats);
   (void)hipFree(c->lights);
+  (void)hipFree(c->smask);
+  c->smask = nullptr;
   c->geom = nullptr;
   c->crad2 = nullptr;
   c->mats = nullptr;
@@ -258,6 +261,15 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   HIP_TRY(hipMemcpy(ctx->mats, mats.data(), mats.size() * sizeof(float),
                     hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(ctx->lights, lg.data(), lg.size() * sizeof(float), hipMemcpyHostToDevice));
+  if (!ps.smask.empty()) {
+    if (hipMalloc(&ctx->smask, ps.smask.size() * sizeof(unsigned)) != hipSuccess) {
+      free_scene(ctx);
+      rtg_set_error("hipMalloc failed for shadow masks");
+      return RTG_ERR_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(ctx->smask, ps.smask.data(), ps.smask.size() * sizeof(unsigned),
+                      hipMemcpyHostToDevice));
+  }
   ctx->n = sphNum;
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
@@ -309,6 +321,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.crad2 = ctx->crad2;
   a.mats = ctx->mats;
   a.lights = ctx->lights;
+  a.smask = ctx->smask;
   a.n = ctx->n;
   a.m = ctx->m;
   a.n4 = ctx->n4;

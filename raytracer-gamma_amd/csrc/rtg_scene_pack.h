@@ -11,6 +11,7 @@
 //   camera constants          main.cpp:384-402
 #pragma once
 
+#include <math.h>
 #include <string.h>
 
 #include <vector>
@@ -21,8 +22,10 @@
 
 namespace rtg {
 
-// Device image of a scene.  geom: n x {x, y, z, r*r} followed by NaN padding
-// records up to n4 + 4 (n4 = n rounded up to 4); crad2: n x (r+1e-6)^2, then
+// Device image of a scene (crad2's third segment, guard_r2, and smask are
+// the shadow-ray masks' data, see shadow_masks).  geom: n x {x, y, z, r*r} followed by NaN padding
+// records up to n4 + 4 (n4 = n rounded up to 4), then the same n4 + 4 records
+// with the pass-1 screen radius^2 (screen_r2) in place of r*r; crad2: n x (r+1e-6)^2, then
 // n x the primary-ray c term |0 - c|^2 - r^2 (same float operations and order
 // as the query's vdot(disp, disp) - r2 with disp = 0 - c, exact negation);
 // mats: (n+1) x {matte.xyz, gloss.xyz, opacity, n} with [n] = background
@@ -30,9 +33,107 @@ namespace rtg {
 // lights: m x {pos.xyz, col.xyz}.  Arrays are never empty (padded to 1).
 struct PackedScene {
   std::vector<float> geom, crad2, mats, lights;
+  // Shadow-ray sphere masks (shadow_masks below): m x n x {lo, hi} words for
+  // 1 <= n <= 64, m >= 1 and a finite scene; empty otherwise (every sphere is
+  // then tested).
+  std::vector<unsigned> smask;
   unsigned n = 0, m = 0;
-  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds n4 + 4 records
+  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 2 x (n4 + 4) records
 };
+
+// Shadow-ray sphere masks.  A shadow ray of raytracer.h:272-309 starts at the
+// hit point P of sphere h and ends at light l.  The kernel first checks that
+// P lies in the guard ball B_h = ball(c_h, g_h) (guard_radius; the computed
+// hit point is within a few ulps of the surface except after near-tangent
+// hits), so the segment P -> L_l lies in the capsule of radius g_h around the
+// segment c_h -> L_l (the capsule contains the convex hull of B_h and L_l).
+// Sphere i can block only if the reference's root test accepts a root t in
+// (1e-5, 1000) with |t D|^2 < |L - P|^2.  The reference's radicand carries a
+// rounding error below ~14 eps a (|p|^2 + r_i^2) (p = P - c_i), so a line
+// that misses ball i by mu can only look like a hit when mu^2 < 14 eps |p|^2,
+// and computed roots move by less than sqrt(14 eps) (|p| + r_i) ~ 1e-3 (|p| +
+// r_i); both are far below the margin
+//   mu_i = 2^-8 (|c_i - c_h| + g_h + r_i) + 2^-16 (|L_l - c_h| + g_h)
+// (the second term covers the ~eps direction error of vnorm(L - P) over the
+// segment).  So if ball i grown by mu_i misses the capsule, every point of
+// the segment is more than r_i + mu_i from c_i: the radicand near the segment
+// stays negative and roots of the line outside the segment keep their side
+// of 0 and of |L - P|, i.e. sphere i never blocks.  Bit i of mask (l, h) is
+// set for i == h and for every sphere whose grown ball meets the capsule
+// (double arithmetic with a further 1e-9 relative slack).  The kernel tests
+// the union of its lanes' masks, and every sphere for a lane whose P fails
+// the guard.  tests/test_oracle.py checks the superset property against the
+// reference's own test on random segments and the kernel's frames bit for bit.
+inline double guard_radius(const rtg_sphere& s) {
+  const double r = fabs((double)s.radius);
+  const double c = fabs((double)s.pos.x) + fabs((double)s.pos.y) + fabs((double)s.pos.z);
+  return r * (1.0 + 0x1p-10) + 0x1p-20 * (c + r);
+}
+
+// g_h^2 (1 - 2^-20) rounded down: the float test |P - c_h|^2 <= guard_r2
+// (relative error < 6 eps) then implies |P - c_h| <= g_h.  -1 (never passes)
+// for non-finite or tiny spheres.
+inline float guard_r2(const rtg_sphere& s) {
+  const double g = guard_radius(s);
+  if (!(g >= 0x1p-60 && g <= 0x1p60)) return -1.f;
+  const double v = g * g * (1.0 - 0x1p-20);
+  float f = (float)v;
+  if ((double)f > v) f = nextafterf(f, 0.f);
+  return f;
+}
+
+inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
+                         unsigned m, std::vector<unsigned>* out) {
+  out->clear();
+  if (n == 0 || n > 64 || m == 0) return;
+  auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
+  for (unsigned i = 0; i < n; ++i)
+    if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
+        !finite(spheres[i].radius))
+      return;
+  for (unsigned l = 0; l < m; ++l)
+    if (!finite(lights[l].pos.x) || !finite(lights[l].pos.y) || !finite(lights[l].pos.z))
+      return;
+  out->assign((size_t)m * n * 2, 0u);
+  for (unsigned l = 0; l < m; ++l) {
+    const double L[3] = {lights[l].pos.x, lights[l].pos.y, lights[l].pos.z};
+    for (unsigned h = 0; h < n; ++h) {
+      const rtg_sphere& sh = spheres[h];
+      const double A[3] = {sh.pos.x, sh.pos.y, sh.pos.z};
+      const double g = guard_radius(sh);
+      double ab[3], ab2 = 0.0;
+      for (int k = 0; k < 3; ++k) { ab[k] = L[k] - A[k]; ab2 += ab[k] * ab[k]; }
+      const double lh = sqrt(ab2);
+      unsigned* w = &(*out)[((size_t)l * n + h) * 2];
+      for (unsigned i = 0; i < n; ++i) {
+        bool keep = (i == h);
+        if (!keep) {
+          const rtg_sphere& si = spheres[i];
+          const double C[3] = {si.pos.x, si.pos.y, si.pos.z};
+          const double ri = fabs((double)si.radius);
+          double t = 0.0, dch = 0.0;
+          for (int k = 0; k < 3; ++k) {
+            const double ca = C[k] - A[k];
+            t += ca * ab[k];
+            dch += ca * ca;
+          }
+          dch = sqrt(dch);
+          t = ab2 > 0.0 ? t / ab2 : 0.0;
+          t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+          double d2 = 0.0;
+          for (int k = 0; k < 3; ++k) {
+            const double e = C[k] - (A[k] + t * ab[k]);
+            d2 += e * e;
+          }
+          const double mu = 0x1p-8 * (dch + g + ri) + 0x1p-16 * (lh + g);
+          const double reach = (g + ri + mu) * (1.0 + 1e-9);
+          keep = !(sqrt(d2) > reach);
+        }
+        if (keep) w[i >> 5] |= 1u << (i & 31);
+      }
+    }
+  }
+}
 
 inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                        unsigned m, PackedScene* ps) {
@@ -40,8 +141,8 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   ps->m = m;
   ps->n4 = (n + 3u) & ~3u;
   // Padding records are NaN spheres: their radicand is NaN, never >= 0.
-  ps->geom.assign((size_t)(ps->n4 + 4) * 4, __builtin_nanf(""));
-  ps->crad2.assign(n ? 2 * (size_t)n : 1, 0.f);
+  ps->geom.assign((size_t)(ps->n4 + 4) * 8, __builtin_nanf(""));
+  ps->crad2.assign(n ? 3 * (size_t)n : 1, 0.f);
   ps->mats.assign((size_t)(n + 1) * 8, 0.f);
   ps->lights.assign((size_t)(m ? m : 1) * 6, 0.f);
   for (unsigned i = 0; i < n; ++i) {
@@ -49,10 +150,14 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     float* g = &ps->geom[(size_t)i * 4];
     g[0] = s.pos.x; g[1] = s.pos.y; g[2] = s.pos.z;
     g[3] = s.radius * s.radius;
+    float* gs = &ps->geom[(size_t)(ps->n4 + 4 + i) * 4];
+    gs[0] = g[0]; gs[1] = g[1]; gs[2] = g[2];
+    gs[3] = screen_r2(g[3]);
     const float rc = s.radius + 1.0e-6f;
     ps->crad2[i] = rc * rc;
     const float dx = 0.f - s.pos.x, dy = 0.f - s.pos.y, dz = 0.f - s.pos.z;
     ps->crad2[n + i] = (((dx * dx) + (dy * dy)) + (dz * dz)) - g[3];
+    ps->crad2[2 * (size_t)n + i] = guard_r2(s);
     float* mt = &ps->mats[(size_t)i * 8];
     mt[0] = s.material.matteColour.x; mt[1] = s.material.matteColour.y;
     mt[2] = s.material.matteColour.z; mt[3] = s.material.glossColour.x;
@@ -60,6 +165,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     mt[6] = s.material.opacity; mt[7] = s.material.refractiveIndex;
   }
   ps->mats[(size_t)n * 8 + 7] = 1.00f;
+  shadow_masks(spheres, n, lights, m, &ps->smask);
   for (unsigned l = 0; l < m; ++l) {
     float* p = &ps->lights[(size_t)l * 6];
     p[0] = lights[l].pos.x; p[1] = lights[l].pos.y; p[2] = lights[l].pos.z;

@@ -117,7 +117,7 @@ struct Frame {
 struct RayQ {
   V3 o, d;
   float a4, den, y;
-  float ap, app;  // pass-1 screen: a (1 - K) and 2 K a, K = 2^-16 (pass1_rad)
+  float ap;       // pass-1 screen: a (1 - K), K = 2^-16 (pass1_rad)
   bool fast;
 };
 
@@ -129,7 +129,6 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.a4 = 4.0f * a;
   q.den = 2.0f * a;
   q.ap = a * (1.0f - 0x1p-16f);
-  q.app = a * 0x1p-15f;
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
   q.y = 1.0f / q.den;
   return q;
@@ -219,10 +218,15 @@ template <int Q, class Scene>
 RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t);
 template <int Q, class Scene>
 RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap);
+template <class Scene>
+RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel);
 
 // raytracer.h:313-367, with the incidence test hoisted ahead of the shadow ray.
+// Q == 4: shadow rays test only the union of the wave's shadow masks
+// (shadow_masks, rtg_scene_pack.h) for the hit sphere `hit`; `guardOK` tells
+// that P lies in that sphere's guard ball (else every sphere is tested).
 template <int Q, class Scene>
-RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
+RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = false) {
   V3 sum = v3(0.f, 0.f, 0.f);
   const unsigned m = sc.m;
   for (unsigned l = 0; l < m; ++l) {
@@ -234,7 +238,15 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N) {
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
       sc.probe_begin(kProbeShadow);
-      const bool blk = query_blocked<Q>(sc, P, dir, gap);
+      bool blk;
+      if constexpr (Q == 4) {
+        if (sc.has_smask())
+          blk = blocked_sel(sc, P, dir, gap, sc.shadow_union(l, hit, guardOK));
+        else
+          blk = query_blocked<2>(sc, P, dir, gap);
+      } else {
+        blk = query_blocked<Q>(sc, P, dir, gap);
+      }
       sc.probe_end(kProbeShadow);
       if (!blk) {
         const float intensity = incidence / gap;
@@ -355,7 +367,12 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         V3 tmp = vmul(I, mh.matte);
         tmp = vsmul(op, tmp);
         sc.probe_begin(kProbeMatte);
-        const V3 mc = matte_light<Q>(sc, P, N);
+        bool guardOK = false;
+        if constexpr (Q == 4) {  // P in the hit sphere's guard ball (shadow masks)
+          const V3 e = vsub(P, c);
+          guardOK = vdot(e, e) <= sc.guard_r2((unsigned)hit);
+        }
+        const V3 mc = matte_light<Q>(sc, P, N, hit, guardOK);
         sc.probe_end(kProbeMatte);
         tmp = vmul(mc, tmp);
         colour = vadd(tmp, colour);
@@ -519,22 +536,35 @@ RTG_HD unsigned push_sign(unsigned acc, float v) {
 // Pass-1 screen for one sphere: a value whose sign bit is clear whenever the
 // reference's radicand test (raytracer.h:99-108, ray_sphere above) accepts.
 // With p = o - c (the same float subtraction as the reference), x = d.p and
-// cc = |p|^2 - r^2 evaluated with fused multiply-adds, it returns
-//   x^2 - a cc (1 - K) + 2 K a r^2 + 2^-100  =  x^2 - a cc + K a (|p|^2 + r^2) + tiny,
+// cs = |p|^2 - rs evaluated with fused multiply-adds, where rs is the
+// sphere's SCREEN radius^2 (screen_r2: r^2 (1 + K) / (1 - K) rounded up,
+// precomputed on the host), it returns
+//   x^2 - a (1 - K) cs + 2^-100  >=  x^2 - a cc + K a (|p|^2 + r^2) + tiny,
 // i.e. the true radicand / 4 plus a slack of K = 2^-16 relative to its terms'
 // magnitude a (|p|^2 + r^2).  Both this and the reference's own evaluation
 // are within ~40 ulps of those magnitudes of the exact value, so the slack
 // (2^8 ulps) covers both: a sphere the reference accepts always passes; the
 // few near-tangent extras are rejected by pass 2's exact test.  The 2^-100
-// floor keeps the screen open where the terms underflow.  13 VALU ops per
-// sphere instead of 19; tests/test_oracle.py checks the superset property
-// on adversarial near-tangent cases.
-RTG_HD float pass1_rad(const RayQ& q, V3 c, float r2) {
+// floor keeps the screen open where the terms underflow.  12 VALU ops per
+// sphere (3 sub, 3 for x, 3 for cs, 2 fma, 1 sign shift) instead of the
+// reference's 19; tests/test_oracle.py checks the superset property on
+// adversarial near-tangent cases.
+RTG_HD float pass1_rad(const RayQ& q, V3 c, float rs) {
   const V3 p = vsub(q.o, c);
   const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
-  const float cc = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -r2)));
-  const float t = fmaf(q.app, r2, 0x1p-100f);
-  return fmaf(x, x, fmaf(-q.ap, cc, t));
+  const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rs)));
+  return fmaf(x, x, fmaf(-q.ap, cs, 0x1p-100f));
+}
+
+// Screen radius^2 of pass1_rad, computed once per sphere on the host:
+// r2 (1 + 2K + 4K^2) >= r2 (1 + K) / (1 - K) in double, rounded up to float
+// (NaN stays NaN, overflow goes to +inf: both keep the screen open).
+inline float screen_r2(float r2) {
+  const double K = 1.0 / 65536.0;
+  const double v = (double)r2 * (1.0 + 2.0 * K + 4.0 * K * K);
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, __builtin_inff());
+  return f;
 }
 
 template <class Scene>
@@ -545,7 +575,7 @@ RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, con
   for (int k = (int)((cnt + 3u) & ~3u) - 4; k >= 0; k -= 4) {
     V3 c[4];
     float r2[4];
-    sc.sphere4(base + (unsigned)k, c, r2);
+    sc.sphere4_screen(base + (unsigned)k, c, r2);
 #pragma unroll
     for (int j = 3; j >= 0; --j) neg = push_sign(neg, pass1_rad(q, c[j], r2[j]));
   }
@@ -595,6 +625,46 @@ RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
+      float r2;
+      const V3 c = sc.sphere_lane(i, r2);
+      bool res;
+      const float t = ray_sphere(q, c, r2, res);
+      if (res && t < 1000.f) {
+        const V3 dist = vsmul(t, d);
+        if (vdot(dist, dist) < gap) return true;
+      }
+    }
+  }
+  return false;
+}
+
+// All-ones when the sign bit of v is set, else 0.
+RTG_HD unsigned sign_mask(float v) {
+  int32_t i;
+  memcpy(&i, &v, 4);
+  return (unsigned)(i >> 31);
+}
+
+// Shadow query over a wave-uniform subset `sel` of spheres 0..63 (the union
+// of the wave's shadow masks): pass 1 screens only the spheres of `sel`, in
+// increasing index order, one scalar load per sphere; pass 2 as blocked_mask.
+// Spheres outside `sel` cannot block (shadow_masks), so the answer equals
+// blocked_mask's, which equals the reference's hasClearLineOfSight.
+template <class Scene>
+RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
+  const RayQ q = make_query(o, d);
+  for (unsigned base = 0; base < 64u; base += 32u) {
+    const unsigned u = (unsigned)(sel >> base);
+    unsigned cand = 0;
+    for (unsigned mm = u; mm; mm &= mm - 1) {  // wave-uniform
+      const unsigned k = (unsigned)__builtin_ctz(mm);
+      float rs;
+      const V3 c = sc.sphere_screen(base + k, rs);
+      cand |= (1u << k) & ~sign_mask(pass1_rad(q, c, rs));
+    }
+    while (cand) {
+      const unsigned i = base + (unsigned)lowest_bit(cand);
+      cand &= cand - 1;
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;

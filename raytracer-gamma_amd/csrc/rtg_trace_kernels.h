@@ -35,6 +35,7 @@ constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 #define RTG_CONST
 #endif
 typedef const RTG_CONST float* cfloat_p;
+typedef const RTG_CONST unsigned* cuint_p;
 
 // Per-lane frame colours in LDS: level lv of thread t at lfr[lv * kBlock + t]
 // (16-byte records, so a wave's ds_read_b128 covers 1 KiB contiguously and is
@@ -75,6 +76,7 @@ struct DevScene {
   MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)
   const float4* lgeom;  // LDS copy of geom (or the global array when it does not fit)
   cfloat_p lights;
+  cuint_p smask;  // m x n x {lo, hi} shadow masks, or null
   unsigned n, m;
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
@@ -91,6 +93,32 @@ struct DevScene {
       c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
       r2[k] = g[4 * k + 3];
     }
+  }
+  // The same with the pass-1 screen radius^2 (second half of geom).
+  __device__ __forceinline__ void sphere4_screen(unsigned i, V3* c, float* rs) const {
+    sphere4(n4 + 4 + i, c, rs);
+  }
+  __device__ __forceinline__ V3 sphere_screen(unsigned i, float& rs) const {
+    return sphere(n4 + 4 + i, rs);
+  }
+  // Shadow masks (rtg_scene_pack.h shadow_masks): present for n <= 64.
+  __device__ __forceinline__ bool has_smask() const { return smask != nullptr; }
+  __device__ __forceinline__ float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
+  // Union of the active lanes' masks for light l (wave-uniform): one pass per
+  // distinct hit sphere among the lanes; every sphere if a lane's hit point
+  // failed its guard test.
+  __device__ __forceinline__ uint64_t shadow_union(unsigned l, int hit, bool guardOK) const {
+    if (__ballot(!guardOK)) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+    uint64_t todo = __ballot(1);
+    uint64_t u = 0;
+    while (todo) {
+      const int src = __builtin_ctzll(todo);
+      const int h0 = __builtin_amdgcn_readlane(hit, src);
+      const cuint_p w = smask + 2u * (l * n + (unsigned)h0);
+      u |= (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      todo &= ~__ballot(hit == h0);
+    }
+    return u;
   }
   // Per-lane sphere record (divergent index): from the LDS copy.
   __device__ __forceinline__ V3 sphere_lane(unsigned i, float& r2) const {
@@ -126,6 +154,7 @@ struct KernelArgs {
   const float* crad2;
   const float* mats;
   const float* lights;
+  const unsigned* smask;  // shadow masks (PackedScene::smask) or null
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
@@ -174,6 +203,7 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.geom = (cfloat_p)a.geom;
   sc.crad2 = (cfloat_p)a.crad2;
   sc.lights = (cfloat_p)a.lights;
+  sc.smask = (cuint_p)a.smask;
   sc.n = a.n;
   sc.m = a.m;
   sc.n4 = a.n4;
@@ -289,7 +319,7 @@ void trace_kernel(const KernelArgs a) {
 // Requires nAA^2 <= 64; the host launches the default kernel otherwise.
 // Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
 // rows, all their samples) traced by one wave, entered converged.
-template <int S, class Sc>
+template <int S, int Q, class Sc>
 __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
@@ -337,7 +367,7 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   }
   V3 c = v3(0.f, 0.f, 0.f);
   if (valid) {
-    c = trace_sample<S, 2>(sc, dir, sc.frames(), usePrim, primSel);
+    c = trace_sample<S, Q>(sc, dir, sc.frames(), usePrim, primSel);
     c = vsmul(a.cam.inv, c);
   }
   // Ordered per-pixel sum (whole wave converged again).
@@ -373,7 +403,8 @@ void trace_samples_kernel(const KernelArgs a) {
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  trace_group<S>(a, sc, gw);
+  // variant 15: the previous default (shadow rays screen every sphere)
+  trace_group<S, (kVariant == 15 ? 2 : 4)>(a, sc, gw);
   record_wave(a, t0, gw);
 }
 
@@ -393,7 +424,7 @@ void trace_samples_kernel(const KernelArgs a) {
 //     pixel (per-sample recursion + two-pass candidate-mask queries + per-wave
 //     primary cull), 7 waves/SIMD; the default until the sample-parallel kernel
 //   14 as 0 with four-wave workgroups
-//   15 same kernel as 0 (kept as an alias for A/B scripts)
+//   15 as 0 with shadow rays screening every sphere (no shadow masks)
 //   16 as 17 with two-wave workgroups
 //   17 as 0 with the materials/geometry staged in LDS per workgroup
 //   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)

@@ -42,6 +42,17 @@ struct HostScene {
   void sphere4(unsigned i, rtg::V3* c, float* r2) const {
     for (int k = 0; k < 4; ++k) c[k] = sphere(i + k, r2[k]);
   }
+  void sphere4_screen(unsigned i, rtg::V3* c, float* rs) const { sphere4(n4 + 4 + i, c, rs); }
+  rtg::V3 sphere_screen(unsigned i, float& rs) const { return sphere(n4 + 4 + i, rs); }
+  // shadow masks: a single lane, so the union is that lane's mask
+  const unsigned* smask = nullptr;
+  bool has_smask() const { return smask != nullptr; }
+  float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
+  uint64_t shadow_union(unsigned l, int hit, bool guardOK) const {
+    if (!guardOK) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+    const unsigned* w = smask + 2u * (l * n + (unsigned)hit);
+    return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  }
   float contain_r2(unsigned i) const { return crad2[i]; }
   float origin_c(unsigned i) const { return crad2[n + i]; }
   rtg::Mat mat(int i) const {
@@ -75,12 +86,14 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 5: p = rtg::shade_pixel<S, 2, false>(sc, cam, x, y); break;
       case 8: p = rtg::shade_pixel<S, 3, true>(sc, cam, x, y); break;
       case 0:
-      case 14: {  // sample-parallel kernel: samples traced one by one, summed in order
+      case 14:
+      case 15: {  // sample-parallel kernel: samples traced one by one, summed in order
         p = rtg::v3(0.f, 0.f, 0.f);
         for (int s = 0; s < cam.nAA * cam.nAA; ++s) {
           float rx, ry;
           const rtg::V3 d = rtg::sample_dir(cam, x, y, s / cam.nAA, s % cam.nAA, rx, ry);
-          rtg::V3 c = rtg::trace_sample<S, 2>(sc, d, sc.frames());
+          rtg::V3 c = g_variant == 15 ? rtg::trace_sample<S, 2>(sc, d, sc.frames())
+                                      : rtg::trace_sample<S, 4>(sc, d, sc.frames());
           c = rtg::vsmul(cam.inv, c);
           p = rtg::vadd(p, c);
         }
@@ -124,6 +137,7 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   rtg::Camera cam;
   if (rtg::make_camera(W, H, zoom, aa, &cam)) return -1;
   HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, m, ps.n4};
+  sc.smask = ps.smask.empty() ? nullptr : ps.smask.data();
   for (unsigned k = 0; k < nrows; ++k) {
     float* o = out + (size_t)k * W * 3;
     switch (S) {
@@ -229,7 +243,7 @@ extern "C" long hostsim_pass1_check(long trials, unsigned long long seed, long* 
     const float cc = rtg::vdot(disp, disp) - r2;
     const float rad = (b * b) - (q.a4 * cc);
     const bool ref = rad >= 0.0f;
-    const float s = rtg::pass1_rad(q, c, r2);
+    const float s = rtg::pass1_rad(q, c, rtg::screen_r2(r2));
     unsigned u;
     memcpy(&u, &s, 4);
     const bool scr = (u >> 31) == 0;
@@ -240,4 +254,120 @@ extern "C" long hostsim_pass1_check(long trials, unsigned long long seed, long* 
   if (accepted) *accepted = acc;
   if (extra) *extra = ext;
   return bad;
+}
+
+// Shadow masks (shadow_masks, rtg_scene_pack.h) against the reference's own
+// blocking test (raytracer.h:272-309 with ray_sphere = raytracer.h:81-141):
+// random scenes of `n` spheres, half of them placed just outside the reach of
+// a random (light, sphere h) capsule; for every sphere i NOT in mask (l, h),
+// `points` random hit points P inside h's guard ball (most within 1e-3 of the
+// surface, half of them on the side facing sphere i) must not be blocked by
+// sphere i.  Returns the violations;
+// *tested counts the (P, i) pairs checked.
+extern "C" long hostsim_shadow_mask_check(long scenes, unsigned n, long points,
+                                          unsigned long long seed, long* tested) {
+  unsigned long long st = seed * 0x9E3779B97F4A7C15ull + 7;
+  auto u01 = [&]() {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  };
+  long bad = 0, cnt = 0;
+  std::vector<rtg_sphere> sph(n);
+  rtg_light lg[2];
+  for (long sc = 0; sc < scenes; ++sc) {
+    const double scale = pow(10.0, -2.0 + 4.0 * u01());
+    for (unsigned i = 0; i < n; ++i) {
+      memset(&sph[i], 0, sizeof(rtg_sphere));
+      sph[i].pos.x = (float)((u01() - 0.5) * 24 * scale);
+      sph[i].pos.y = (float)((u01() - 0.5) * 16 * scale);
+      sph[i].pos.z = (float)((-6 - 34 * u01()) * scale);
+      sph[i].radius = (float)((0.3 + 3 * u01()) * scale);
+    }
+    for (int l = 0; l < 2; ++l) {
+      lg[l].pos.x = (float)((u01() - 0.5) * 120 * scale);
+      lg[l].pos.y = (float)((10 + 70 * u01()) * scale);
+      lg[l].pos.z = (float)((u01() - 0.5) * 130 * scale);
+    }
+    // half of the spheres: just outside (or on) the capsule of (light 0, sphere 0)
+    for (unsigned i = n / 2; i < n; ++i) {
+      const rtg_sphere& h = sph[0];
+      const double t = (i & 1) ? u01() : 0.05 * u01() * u01();  // mostly near sphere 0
+      const double A[3] = {h.pos.x, h.pos.y, h.pos.z};
+      const double L[3] = {lg[0].pos.x, lg[0].pos.y, lg[0].pos.z};
+      double p[3], ab[3];
+      for (int k = 0; k < 3; ++k) { ab[k] = L[k] - A[k]; p[k] = A[k] + t * ab[k]; }
+      // a unit vector orthogonal to ab
+      double v[3] = {u01() - 0.5, u01() - 0.5, u01() - 0.5};
+      const double ab2 = ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2];
+      const double pr = (v[0] * ab[0] + v[1] * ab[1] + v[2] * ab[2]) / ab2;
+      for (int k = 0; k < 3; ++k) v[k] -= pr * ab[k];
+      const double vl = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      const double ri = sph[i].radius;
+      const double g = rtg::guard_radius(h);
+      const double dist = (g + ri) * (1.0 + pow(10.0, -4.0 + 2.5 * u01()));
+      sph[i].pos.x = (float)(p[0] + dist * v[0] / vl);
+      sph[i].pos.y = (float)(p[1] + dist * v[1] / vl);
+      sph[i].pos.z = (float)(p[2] + dist * v[2] / vl);
+    }
+    std::vector<unsigned> masks;
+    rtg::shadow_masks(sph.data(), n, lg, 2, &masks);
+    if (masks.empty()) continue;
+    for (int l = 0; l < 2; ++l)
+      for (unsigned h = 0; h < n; ++h) {
+        const unsigned* w = &masks[((size_t)l * n + h) * 2];
+        const rtg_sphere& sh = sph[h];
+        const double g = rtg::guard_radius(sh);
+        const float G2 = rtg::guard_r2(sh);
+        for (unsigned i = 0; i < n; ++i) {
+          if (w[i >> 5] & (1u << (i & 31))) continue;
+          for (long k = 0; k < points; ++k) {
+            // P inside the guard ball, mostly near the sphere surface, half of
+            // them on the side facing sphere i (grazing shadow rays)
+            double ux = u01() - 0.5, uy = u01() - 0.5, uz = u01() - 0.5;
+            if (k & 1) {
+              const double cx = (double)sph[i].pos.x - sh.pos.x, cy = (double)sph[i].pos.y - sh.pos.y,
+                           cz = (double)sph[i].pos.z - sh.pos.z;
+              const double cl = sqrt(cx * cx + cy * cy + cz * cz) + 1e-300;
+              const double spread = pow(10.0, -3.0 * u01());
+              ux = cx / cl + spread * ux; uy = cy / cl + spread * uy; uz = cz / cl + spread * uz;
+            }
+            const double ul = sqrt(ux * ux + uy * uy + uz * uz);
+            const double rad = (k % 6 == 0) ? g * u01()
+                                             : fabs((double)sh.radius) * (1.0 + (u01() - 0.7) * 2e-3);
+            const rtg::V3 P = rtg::v3((float)(sh.pos.x + rad * ux / ul),
+                                      (float)(sh.pos.y + rad * uy / ul),
+                                      (float)(sh.pos.z + rad * uz / ul));
+            const rtg::V3 e = rtg::vsub(P, rtg::v3(sh.pos.x, sh.pos.y, sh.pos.z));
+            if (!(rtg::vdot(e, e) <= G2)) continue;  // the kernel tests every sphere then
+            const rtg::V3 Lp = rtg::v3(lg[l].pos.x, lg[l].pos.y, lg[l].pos.z);
+            const rtg::V3 dist = rtg::vsub(Lp, P);
+            const float gap = rtg::vdot(dist, dist);
+            const rtg::V3 D = rtg::vsmul(1.f / sqrtf(gap), dist);
+            const rtg::RayQ q = rtg::make_query(P, D);
+            ++cnt;
+            bool res;
+            const float t = rtg::ray_sphere(q, rtg::v3(sph[i].pos.x, sph[i].pos.y, sph[i].pos.z),
+                                            sph[i].radius * sph[i].radius, res);
+            if (res && t < 1000.f) {
+              const rtg::V3 tv = rtg::vsmul(t, D);
+              if (rtg::vdot(tv, tv) < gap) ++bad;
+            }
+          }
+        }
+      }
+  }
+  if (tested) *tested = cnt;
+  return bad;
+}
+
+// Sizes of the shadow masks of a scene: *total = sum of popcounts over the
+// m x n masks (-1 when the scene has none).
+extern "C" long hostsim_shadow_mask_bits(const rtg_sphere* spheres, unsigned n,
+                                         const rtg_light* lights, unsigned m) {
+  std::vector<unsigned> masks;
+  rtg::shadow_masks(spheres, n, lights, m, &masks);
+  if (masks.empty()) return -1;
+  long bits = 0;
+  for (unsigned w : masks) bits += __builtin_popcount(w);
+  return bits;
 }

@@ -132,8 +132,8 @@ def hostsim():
     return ctypes.CDLL(so)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 8, 9],
-                ids=["v0", "v1", "v2", "v3", "v4", "v5", "v8", "v9"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 8, 9, 15],
+                ids=["v0", "v1", "v2", "v3", "v4", "v5", "v8", "v9", "v15"])
 def variant(request, hostsim):
     hostsim.hostsim_set_variant(request.param)
     yield request.param
@@ -246,3 +246,29 @@ def test_pass1_screen_is_a_superset(hostsim):
     assert bad == 0, bad
     assert acc.value > n // 5
     assert ext.value < 0.3 * n, ext.value
+
+
+def test_shadow_masks_are_conservative(hostsim):
+    """A sphere left out of a shadow mask (shadow_masks, rtg_scene_pack.h) never
+    blocks a shadow ray from a hit point inside the guard ball to the light,
+    by the reference's own test (raytracer.h:272-309), over random scenes at
+    scales 1e-2..1e2 with half of the spheres placed just outside the capsule
+    reach (relative gaps 1e-4..3e-2)."""
+    f = hostsim.hostsim_shadow_mask_check
+    f.restype = ctypes.c_long
+    tested = ctypes.c_long(0)
+    bad = f(ctypes.c_long(400), 12, ctypes.c_long(60), ctypes.c_ulonglong(99),
+            ctypes.byref(tested))
+    assert bad == 0, bad
+    assert tested.value > 1_000_000, tested.value
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c4"])
+def test_shadow_masks_cull(hostsim, golden, name):
+    """The masks of the benchmark scenes are small (the point of them)."""
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
+    f = hostsim.hostsim_shadow_mask_bits
+    f.restype = ctypes.c_long
+    bits = f(P(sph), len(sph), P(lg), len(lg))
+    assert 0 < bits <= 0.3 * len(sph) * len(sph) * len(lg), bits
