@@ -290,13 +290,13 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
   if (rc) return rc;
   int variant = ctx->opts.variant;
-  // sample-parallel kernel: needs all of a pixel's samples in one wave
   // sample-parallel kernels need all of a pixel's samples in one wave
-  const bool sampleKernel = variant == 0 || (variant >= 14 && variant <= 17);
-  if (sampleKernel && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = 9;
+  auto isSample = [](int v) { return v == 0 || (v >= 14 && v <= 18) || v == 110; };
+  if (isSample(variant) && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = variant == 110 ? 100 : 9;
+  const bool sampleKernel = isSample(variant);
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
-  if (variant == 0 || variant == 15) ldsMats = false;
+  if (variant == 0 || variant == 15 || variant == 18 || variant == 110) ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {
     rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
@@ -344,8 +344,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   HIP_TRY(hipSetDevice(ctx->device));
   unsigned threads = (unsigned)kBlock;
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
-  if (variant == 0 || (variant >= 14 && variant <= 17)) {
-    const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);
+  if (sampleKernel) {
+    const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
     const size_t waves = ((size_t)width * rows + ppw - 1) / ppw;
     const unsigned tpb = variant == 14 ? 256u : variant == 16 ? 128u : 64u;
     const size_t blocks = (waves + tpb / 64 - 1) / (tpb / 64);

@@ -25,7 +25,8 @@ namespace rtg {
 // Device image of a scene (crad2's third segment, guard_r2, and smask are
 // the shadow-ray masks' data, see shadow_masks).  geom: n x {x, y, z, r*r} followed by NaN padding
 // records up to n4 + 4 (n4 = n rounded up to 4), then the same n4 + 4 records
-// with the pass-1 screen radius^2 (screen_r2) in place of r*r; crad2: n x (r+1e-6)^2, then
+// with the pass-1 screen radius^2 (screen_r2) in place of r*r, then with the
+// containment radius^2 (r + 1e-6f)^2 (primary_container); crad2: n x (r+1e-6)^2, then
 // n x the primary-ray c term |0 - c|^2 - r^2 (same float operations and order
 // as the query's vdot(disp, disp) - r2 with disp = 0 - c, exact negation);
 // mats: (n+1) x {matte.xyz, gloss.xyz, opacity, n} with [n] = background
@@ -38,7 +39,7 @@ struct PackedScene {
   // then tested).
   std::vector<unsigned> smask;
   unsigned n = 0, m = 0;
-  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 2 x (n4 + 4) records
+  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records
 };
 
 // Shadow-ray sphere masks.  A shadow ray of raytracer.h:272-309 starts at the
@@ -141,7 +142,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   ps->m = m;
   ps->n4 = (n + 3u) & ~3u;
   // Padding records are NaN spheres: their radicand is NaN, never >= 0.
-  ps->geom.assign((size_t)(ps->n4 + 4) * 8, __builtin_nanf(""));
+  ps->geom.assign((size_t)(ps->n4 + 4) * 12, __builtin_nanf(""));
   ps->crad2.assign(n ? 3 * (size_t)n : 1, 0.f);
   ps->mats.assign((size_t)(n + 1) * 8, 0.f);
   ps->lights.assign((size_t)(m ? m : 1) * 6, 0.f);
@@ -153,8 +154,11 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     float* gs = &ps->geom[(size_t)(ps->n4 + 4 + i) * 4];
     gs[0] = g[0]; gs[1] = g[1]; gs[2] = g[2];
     gs[3] = screen_r2(g[3]);
+    float* gc = &ps->geom[(size_t)(2 * (ps->n4 + 4) + i) * 4];
+    gc[0] = g[0]; gc[1] = g[1]; gc[2] = g[2];
     const float rc = s.radius + 1.0e-6f;
     ps->crad2[i] = rc * rc;
+    gc[3] = ps->crad2[i];
     const float dx = 0.f - s.pos.x, dy = 0.f - s.pos.y, dz = 0.f - s.pos.z;
     ps->crad2[n + i] = (((dx * dx) + (dy * dy)) + (dz * dz)) - g[3];
     ps->crad2[2 * (size_t)n + i] = guard_r2(s);

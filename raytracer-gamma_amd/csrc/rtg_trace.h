@@ -200,17 +200,37 @@ RTG_HD bool blocked(const Scene& sc, V3 o, V3 d, float gap) {
   return false;
 }
 
-// raytracer.h:245-270
+RTG_HD int lowest_bit(unsigned m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_ctz(m);
+#else
+  return __builtin_ctz(m);
+#endif
+}
+
+// raytracer.h:245-270: the first sphere i whose (r_i + 1e-6)^2 bounds
+// |pt - c_i|^2 (same float operations), or -1.  Four spheres per step (one
+// 64-byte scalar load of containment records {c, (r + 1e-6)^2}, NaN padding
+// past n never matches); the first index is the lowest set bit, and the wave
+// stops once every lane has its answer.
 template <class Scene>
 RTG_HD int primary_container(const Scene& sc, V3 pt) {
-  const unsigned n = sc.n;
-  for (unsigned i = 0; i < n; ++i) {
-    float r2;
-    V3 c = sc.sphere(i, r2);
-    V3 dist = vsub(pt, c);
-    if (vdot(dist, dist) <= sc.contain_r2(i)) return (int)i;
+  int found = -1;
+  const unsigned n4 = sc.n4;
+  for (unsigned k = 0; k < n4; k += 4) {  // wave-uniform
+    V3 c[4];
+    float cr[4];
+    sc.sphere4_contain(k, c, cr);
+    unsigned bits = 0;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+      const V3 dist = vsub(pt, c[j]);
+      bits = (bits << 1) | ((vdot(dist, dist) <= cr[j]) ? 1u : 0u);
+    }
+    if (found < 0 && bits) found = (int)(k + (unsigned)lowest_bit(bits));
+    if (sc.all(found >= 0)) break;
   }
-  return -1;
+  return found;
 }
 
 // Query strategies (defined below): see query_closest / query_blocked.
@@ -583,13 +603,6 @@ RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, con
   return ~neg & all;
 }
 
-RTG_HD int lowest_bit(unsigned m) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_ctz(m);
-#else
-  return __builtin_ctz(m);
-#endif
-}
 
 template <class Scene>
 RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {

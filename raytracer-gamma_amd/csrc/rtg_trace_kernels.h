@@ -98,6 +98,10 @@ struct DevScene {
   __device__ __forceinline__ void sphere4_screen(unsigned i, V3* c, float* rs) const {
     sphere4(n4 + 4 + i, c, rs);
   }
+  // ... and with the containment radius^2 (third part of geom).
+  __device__ __forceinline__ void sphere4_contain(unsigned i, V3* c, float* cr) const {
+    sphere4(2 * (n4 + 4) + i, c, cr);
+  }
   __device__ __forceinline__ V3 sphere_screen(unsigned i, float& rs) const {
     return sphere(n4 + 4 + i, rs);
   }
@@ -176,7 +180,8 @@ __device__ __forceinline__ float canon_nan(float v) {
 template <int S, int kVariant>
 struct MinWaves {
   static constexpr int value =
-      ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
+      (kVariant == 18 && S <= 6) ? 8
+      : ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
 };
 
 // Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
@@ -319,7 +324,7 @@ void trace_kernel(const KernelArgs a) {
 // Requires nAA^2 <= 64; the host launches the default kernel otherwise.
 // Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
 // rows, all their samples) traced by one wave, entered converged.
-template <int S, int Q, class Sc>
+template <int S, int Q, bool kDiag, class Sc>
 __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
@@ -366,9 +371,19 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
     usePrim = true;
   }
   V3 c = v3(0.f, 0.f, 0.f);
+  unsigned long long tk0 = 0;
+  if constexpr (kDiag) {
+    for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
+    tk0 = __builtin_amdgcn_s_memtime();
+  }
   if (valid) {
     c = trace_sample<S, Q>(sc, dir, sc.frames(), usePrim, primSel);
     c = vsmul(a.cam.inv, c);
+  }
+  if constexpr (kDiag) {  // wave converged again: one add per slot
+    sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
+    if ((threadIdx.x & 63u) == 0)
+      for (int k = 0; k < kProbeSlots; ++k) atomicAdd(&a.diag[k], sc.acc[k]);
   }
   // Ordered per-pixel sum (whole wave converged again).
   const unsigned base = pl * SP;
@@ -399,12 +414,12 @@ __global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVaria
 void trace_samples_kernel(const KernelArgs a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, false, kThreads> sc;
+  DevScene<MatPtr, (kVariant >= 100), kThreads> sc;
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screen every sphere)
-  trace_group<S, (kVariant == 15 ? 2 : 4)>(a, sc, gw);
+  trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100)>(a, sc, gw);
   record_wave(a, t0, gw);
 }
 
@@ -425,15 +440,17 @@ void trace_samples_kernel(const KernelArgs a) {
 //     primary cull), 7 waves/SIMD; the default until the sample-parallel kernel
 //   14 as 0 with four-wave workgroups
 //   15 as 0 with shadow rays screening every sphere (no shadow masks)
+//   18 as 0 built for 8 waves per SIMD (<= 64 VGPRs)
 //   16 as 17 with two-wave workgroups
 //   17 as 0 with the materials/geometry staged in LDS per workgroup
 //   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
-//   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9
+//   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9,
+//     110 = the default sample kernel (0)
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15)
+  else if constexpr (V == 0 || V == 15 || V == 18 || V == 110)
     return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -442,6 +459,8 @@ template <int S>
 static TraceFn trace_fn(bool lds, int variant) {
   switch (variant) {
     case 100: return trace_fn_v<S, 100>(lds);
+    case 110: return trace_fn_v<S, 110>(lds);
+    case 18: return trace_fn_v<S, 18>(lds);
     case 104: return trace_fn_v<S, 104>(lds);
     case 1: return trace_fn_v<S, 1>(lds);
     case 4: return trace_fn_v<S, 4>(lds);

@@ -44,6 +44,7 @@ struct HostScene {
   }
   void sphere4_screen(unsigned i, rtg::V3* c, float* rs) const { sphere4(n4 + 4 + i, c, rs); }
   rtg::V3 sphere_screen(unsigned i, float& rs) const { return sphere(n4 + 4 + i, rs); }
+  void sphere4_contain(unsigned i, rtg::V3* c, float* cr) const { sphere4(2 * (n4 + 4) + i, c, cr); }
   // shadow masks: a single lane, so the union is that lane's mask
   const unsigned* smask = nullptr;
   bool has_smask() const { return smask != nullptr; }
