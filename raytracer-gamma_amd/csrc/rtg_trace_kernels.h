@@ -441,6 +441,8 @@ void trace_samples_kernel(const KernelArgs a) {
 //   14 as 0 with four-wave workgroups
 //   15 as 0 with shadow rays screening every sphere (no shadow masks)
 //   18 as 0 built for 8 waves per SIMD (<= 64 VGPRs)
+//   (19-21, persistent sample kernels with static / atomic-queue dealing of
+//    pixel groups, were removed: register spills made them slower)
 //   16 as 17 with two-wave workgroups
 //   17 as 0 with the materials/geometry staged in LDS per workgroup
 //   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
