@@ -34,9 +34,9 @@ namespace rtg {
 // lights: m x {pos.xyz, col.xyz}.  Arrays are never empty (padded to 1).
 struct PackedScene {
   std::vector<float> geom, crad2, mats, lights;
-  // Shadow-ray sphere masks (shadow_masks below): m x n x {lo, hi} words for
-  // 1 <= n <= 64, m >= 1 and a finite scene; empty otherwise (every sphere is
-  // then tested).
+  // Sphere masks (shadow_masks below): m x n shadow masks, then n overlap
+  // masks, each {lo, hi} words, for 1 <= n <= 64 and a finite scene; empty
+  // otherwise (every sphere is then tested).
   std::vector<unsigned> smask;
   unsigned n = 0, m = 0;
   unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records
@@ -86,7 +86,7 @@ inline float guard_r2(const rtg_sphere& s) {
 inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                          unsigned m, std::vector<unsigned>* out) {
   out->clear();
-  if (n == 0 || n > 64 || m == 0) return;
+  if (n == 0 || n > 64) return;
   auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
   for (unsigned i = 0; i < n; ++i)
     if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
@@ -95,7 +95,7 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
   for (unsigned l = 0; l < m; ++l)
     if (!finite(lights[l].pos.x) || !finite(lights[l].pos.y) || !finite(lights[l].pos.z))
       return;
-  out->assign((size_t)m * n * 2, 0u);
+  out->assign(((size_t)m * n + n) * 2, 0u);
   for (unsigned l = 0; l < m; ++l) {
     const double L[3] = {lights[l].pos.x, lights[l].pos.y, lights[l].pos.z};
     for (unsigned h = 0; h < n; ++h) {
@@ -132,6 +132,27 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
         }
         if (keep) w[i >> 5] |= 1u << (i & 31);
       }
+    }
+  }
+  // Overlap masks (closest_enter, rtg_trace.h): bit j of mask h is set when
+  // ball j grown by mu_j = 2^-8 (|c_j - c_h| + g_h + r_j) meets the guard ball
+  // B_h.  A ray whose origin and computed exit point from sphere h both lie in
+  // B_h stays inside B_h up to that exit, so a sphere outside the mask has no
+  // accepted root before it (same error argument as above): the closest hit
+  // is h or an overlap sphere.
+  for (unsigned h = 0; h < n; ++h) {
+    const rtg_sphere& sh = spheres[h];
+    const double g = guard_radius(sh);
+    unsigned* w = &(*out)[((size_t)m * n + h) * 2];
+    for (unsigned j = 0; j < n; ++j) {
+      if (j == h) continue;
+      const rtg_sphere& sj = spheres[j];
+      const double dx = (double)sj.pos.x - sh.pos.x, dy = (double)sj.pos.y - sh.pos.y,
+                   dz = (double)sj.pos.z - sh.pos.z;
+      const double d = sqrt(dx * dx + dy * dy + dz * dz);
+      const double rj = fabs((double)sj.radius);
+      const double mu = 0x1p-8 * (d + g + rj);
+      if (!(d > (g + rj + mu) * (1.0 + 1e-9))) w[j >> 5] |= 1u << (j & 31);
     }
   }
 }

@@ -359,6 +359,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
   V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
   int rm = (int)sc.n;                   // background material
+  int enterH = -1;  // Q == 4: the sphere this ray entered (refraction child), or -1
   for (;;) {
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
@@ -367,9 +368,15 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     if (usePrim) {  // the primary ray: only spheres its wave's bundle can reach
       hit = closest_hit_sel(sc, o, d, t, primSel);
       usePrim = false;
+    } else if (Q == 4 && sc.has_smask() && sc.all(enterH >= 0)) {
+      // every active lane traces a ray that entered a sphere: try h + overlaps
+      bool ok;
+      hit = closest_enter(sc, make_query(o, d), enterH, t, ok);
+      if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
     } else {
-      hit = query_closest<Q>(sc, o, d, t);
+      hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
     }
+    enterH = -1;
     sc.probe_end(kProbeClosest);
     sc.probe_begin(kProbeShade);
     if (hit < 0) {
@@ -427,7 +434,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           }
           ++sp;
           ret = colour;                                       // :538
-          // refraction child: calculateRefraction's refracted ray (:805-809)
+          // refraction child: calculateRefraction's refracted ray (:805-809);
+          // hit from outside (cosA1 < 0): the child starts in sphere `hit`
+          if (Q == 4 && vdot(d, N) < 0.f) enterH = hit;
           I = vsmul((1.f - R), vsmul(tr, I));
           o = P;
           d = cdir;
@@ -689,6 +698,47 @@ RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
     }
   }
   return false;
+}
+
+// Closest hit of a ray that starts inside sphere h's guard ball B_h (the
+// refraction child of a hit on h from outside): sphere h's own root test
+// (raytracer.h:81-141) gives t_h; when it is a hit and both the origin and the
+// computed exit point o + t_h d lie in B_h (`ok`), no sphere outside h's
+// overlap mask (shadow_masks, rtg_scene_pack.h) has an accepted root before
+// t_h, so the reference's closest hit (raytracer.h:145-194: strict <, index
+// order) is found among h and its overlap spheres, tested here in index order.
+// When !ok the caller runs the full query.
+template <class Scene>
+RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
+  float r2;
+  const V3 c = sc.sphere_lane((unsigned)h, r2);
+  bool res;
+  const float th = ray_sphere(q, c, r2, res);
+  const V3 e0 = vsub(q.o, c);
+  const V3 e1 = vsub(vadd(q.o, vsmul(th, q.d)), c);
+  const float g2 = sc.guard_r2((unsigned)h);
+  ok = res && th < 1000.f && vdot(e0, e0) <= g2 && vdot(e1, e1) <= g2;
+  float minT = 1000.f;
+  int best = -1;
+  uint64_t ov = ok ? sc.overlap_mask((unsigned)h) : 0ull;
+  bool hDone = false;
+  for (;;) {  // candidates in index order; h's result is already known
+    const unsigned j = ov ? (unsigned)__builtin_ctzll(ov) : 64u;
+    if (!hDone && (unsigned)h < j) {
+      hDone = true;
+      if (th < minT) { minT = th; best = h; }  // res holds when ok
+      continue;
+    }
+    if (j == 64u) break;
+    ov &= ov - 1;
+    float rj2;
+    const V3 cj = sc.sphere_lane(j, rj2);
+    bool rj;
+    const float t = ray_sphere(q, cj, rj2, rj);
+    if (rj && t < minT) { minT = t; best = (int)j; }
+  }
+  tOut = minT;
+  return best;
 }
 
 // Closest hit restricted to a wave-uniform subset `sel` of spheres 0..63

@@ -105,8 +105,12 @@ struct DevScene {
   __device__ __forceinline__ V3 sphere_screen(unsigned i, float& rs) const {
     return sphere(n4 + 4 + i, rs);
   }
-  // Shadow masks (rtg_scene_pack.h shadow_masks): present for n <= 64.
+  // Shadow and overlap masks (rtg_scene_pack.h shadow_masks): n <= 64.
   __device__ __forceinline__ bool has_smask() const { return smask != nullptr; }
+  __device__ __forceinline__ uint64_t overlap_mask(unsigned h) const {  // per lane
+    const cuint_p w = smask + 2u * (m * n + h);
+    return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  }
   __device__ __forceinline__ float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
   // Union of the active lanes' masks for light l (wave-uniform): one pass per
   // distinct hit sphere among the lanes; every sphere if a lane's hit point

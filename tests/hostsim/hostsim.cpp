@@ -48,6 +48,10 @@ struct HostScene {
   // shadow masks: a single lane, so the union is that lane's mask
   const unsigned* smask = nullptr;
   bool has_smask() const { return smask != nullptr; }
+  uint64_t overlap_mask(unsigned h) const {
+    const unsigned* w = smask + 2u * (m * n + h);
+    return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  }
   float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
   uint64_t shadow_union(unsigned l, int hit, bool guardOK) const {
     if (!guardOK) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
@@ -312,7 +316,7 @@ extern "C" long hostsim_shadow_mask_check(long scenes, unsigned n, long points,
     }
     std::vector<unsigned> masks;
     rtg::shadow_masks(sph.data(), n, lg, 2, &masks);
-    if (masks.empty()) continue;
+    if (masks.empty()) continue;  // (m * n shadow masks come first)
     for (int l = 0; l < 2; ++l)
       for (unsigned h = 0; h < n; ++h) {
         const unsigned* w = &masks[((size_t)l * n + h) * 2];
