@@ -65,39 +65,62 @@ def canon_md5(fb: np.ndarray) -> str:
     return hashlib.md5(b.tobytes()).hexdigest()
 
 
+def cpu_threads() -> int:
+    """Host threads for the multi-threaded CPU baseline: the CPUs this process
+    may run on, capped at 16 (the GPU box's CPU share per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(name, sph, lg, W, H, S, budget_s):
-    """Reference CPU path (oracle/_ref, compiled from the reference's
-    raytracer.h) on one host thread over a strided row sample of the same
-    frame; falls back to the C restatement if the reference build is absent."""
+    """The reference CPU path (oracle/_ref, compiled from the reference's own
+    raytracer.h) over a strided row sample of the same frame, on one host
+    thread (the reference's main.cpp:404 loop is single-threaded) and on all
+    host threads with dynamic row scheduling; falls back to
+    the C restatement if the reference build is absent.  Each leg gets half
+    of `budget_s` of wall time.  The multi-threaded figure is the baseline."""
     ref = os.path.join(ROOT, "oracle", "_ref", f"librtgref_S{S}.so")
     port = os.path.join(ROOT, "oracle", "build", "librtg_oracle.so")
     kind = "reference" if os.path.exists(ref) else "port"
     L = ctypes.CDLL(ref if kind == "reference" else port)
     P = lambda a: ctypes.c_void_p(a.ctypes.data) if a.size else None  # noqa: E731
 
-    def run(rows):
+    def run(rows, threads):
         rows = np.asarray(rows, np.uint32)
         out = np.zeros((len(rows), W, 3), np.float32)
         t0 = time.perf_counter()
         if kind == "reference":
             L.ref_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
-                              ctypes.c_float(3.0), P(rows), len(rows), P(out), 1)
+                              ctypes.c_float(3.0), P(rows), len(rows), P(out), threads)
         else:
             L.oracle_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
-                                 ctypes.c_float(3.0), S, P(rows), len(rows), P(out), 1, None)
+                                 ctypes.c_float(3.0), S, P(rows), len(rows), P(out), threads,
+                                 None)
         return time.perf_counter() - t0, out
 
-    # calibrate on a 1/64 stride, then pick the stride that fits the budget
-    t_cal, _ = run(range(0, H, 64))
-    est_full = t_cal * 64
-    stride = max(1, int(np.ceil(est_full / budget_s)))
-    rows = list(range(0, H, stride))
-    t, out = run(rows)
-    px = len(rows) * W
-    return {"value": round(px / t / 1e6, 5), "unit": "Mpixels/s", "cores": 1, "kind": kind,
-            "sample": f"{name} rows 0,{stride},{2 * stride},... ({len(rows)} of {H} rows, "
-                      f"{px} px, {t:.1f} s, 1 thread)",
-            "frame_s_extrapolated": round(t * H / len(rows), 1)}, rows, out
+    def leg(threads, budget):
+        # calibrate on a 1/64 stride, then pick the stride that fits the budget
+        t_cal, _ = run(range(0, H, 64), threads)
+        stride = max(1, int(np.ceil(t_cal * 64 / budget)))
+        rows = list(range(0, H, stride))
+        t, out = run(rows, threads)
+        px = len(rows) * W
+        return {"value": round(px / t / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
+                "kind": kind,
+                "sample": f"{name} rows 0,{stride},{2 * stride},... ({len(rows)} of {H} rows, "
+                          f"{px} px, {t:.1f} s, {threads} thread{'s' if threads > 1 else ''})",
+                "frame_s_extrapolated": round(t * H / len(rows), 1)}, rows, out
+
+    T = cpu_threads()
+    one, rows, out = leg(1, budget_s / 2)
+    if T > 1:
+        multi, rows_m, out_m = leg(T, budget_s / 2)
+        multi["single_thread"] = one
+        return multi, rows + rows_m, np.concatenate([out, out_m])
+    return one, rows, out
 
 
 def main():
@@ -113,7 +136,8 @@ def main():
     ap.add_argument("--ab-rounds", type=int, default=5)
     ap.add_argument("--diag", type=int, default=0, help="diagnostic variant (e.g. 102) to run "
                     "once after timing; reports s_memtime cycle shares per phase")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
+    ap.add_argument("--cpu-budget", type=float, default=16.0,
+                    help="seconds of CPU baseline (split between the 1-thread and all-thread legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather-chunks", type=int, default=4,
                     help="N > 1: split each rank's rows into K chunks; each chunk is rendered "
@@ -339,6 +363,8 @@ def main():
             if rec.get("source_md5") == mod.source_md5() and rec.get("variant") == args.variant \
                     and "traffic_bytes" in rec:
                 roof["traffic"] = int(rec["traffic_bytes"])
+                if "valu_issue_utilisation" in rec:
+                    roof["valu_issue_utilisation_pmc"] = round(rec["valu_issue_utilisation"], 3)
                 roof["traffic_note"] = ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
                                         f"({pmc}); mostly private-memory reflection rays")
 

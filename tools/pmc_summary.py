@@ -47,6 +47,14 @@ def main():
         u = avg["SQ_THREAD_CYCLES_VALU"] / (avg["SQ_ACTIVE_INST_VALU"] * 64)
         out["valu_lane_utilisation"] = u
         print("VALU lane utilisation       %.3f" % u)
+    if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles; 1024 SIMDs issue one
+        # wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md)
+        cyc = avg["GRBM_GUI_ACTIVE"] / 8
+        out["valu_issue_utilisation"] = avg["SQ_INSTS_VALU"] / (1024 * cyc / 2)
+        out["busy_ms_at_2p4GHz"] = cyc / 2.4e6
+        print("VALU issue utilisation      %.3f  (%.3g wave instructions / %.3g slots)" % (
+            out["valu_issue_utilisation"], avg["SQ_INSTS_VALU"], 1024 * cyc / 2))
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         rd = avg["FETCH_SIZE"] * 2 * 1024
         wr = avg["WRITE_SIZE"] * 1024
