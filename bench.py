@@ -176,6 +176,8 @@ def main():
     shard = torch.zeros((Rmax, W, 3), dtype=torch.float32, device="cuda")
     gathered = (torch.empty((world, Rmax, W, 3), dtype=torch.float32, device="cuda")
                 if (world > 1 and rank == 0) else None)
+    frame_buf = (torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+                 if (world > 1 and rank == 0) else None)
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
     ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -223,7 +225,12 @@ def main():
         for w in works:
             w.wait()
         if rank == 0:
-            frame = rdist.assemble(gathered, H, B).contiguous()
+            if args.dist_backend == "nccl":  # native permute kernel on the device
+                ctx.assemble_shards_device(gathered.data_ptr(), world, Rmax, W, H, B,
+                                           frame_buf.data_ptr(), stream=sptr)
+                frame = frame_buf
+            else:
+                frame = rdist.assemble(gathered, H, B).contiguous()
 
     for _ in range(args.warmup):
         step()

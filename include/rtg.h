@@ -17,6 +17,7 @@
  *                                                      rtg_max_colour_device
  *   savePPM  main.cpp:43-91                            rtg_save_ppm / rtg_ppm_bytes
  *   rayTrace(...)  raytracer.h:410-636 (CPU entry)     (inside the HIP kernel)
+ *   (8-GPU node, SURVEY.md §8e: none in the reference) rtg_render_multi (RCCL gather)
  *   checkError -> exit(EXIT_FAILURE)  err_code.h:143   negative return + rtg_last_error
  *   output_device_info  device_info.cpp:30             rtg_device_info
  *   parseArguments --list/--device  device_picker.h:70 rtg_device_count / device index args
@@ -89,6 +90,19 @@ int rtg_render(int device, const rtg_sphere* spheres, unsigned sphNum,
                unsigned height, float zoom, float aliasFactor, int stackSize,
                rtg_vec* dstHost);
 
+/* ---- multi-GPU one-shot: one process, nDevices GPUs ----
+ * `devices` lists distinct device ids; devices[0] is the root.  Rows are dealt
+ * row-cyclically in blocks of rowBlock (16 is a good default); every device
+ * renders its shard on its own stream, ONE grouped RCCL gather (ncclGather)
+ * brings the shards to the root over xGMI, the root restores row order
+ * (rtg_assemble_shards_device) and W*H rtg_vec are copied to dstHost.
+ * Bit-identical to rtg_render.  timingsMs (optional, 3 floats): slowest
+ * device's render, gather + assemble on the root, wall time of the call. */
+int rtg_render_multi(const int* devices, int nDevices, const rtg_sphere* spheres,
+                     unsigned sphNum, const rtg_light* lights, unsigned lgtNum,
+                     unsigned width, unsigned height, float zoom, float aliasFactor,
+                     int stackSize, unsigned rowBlock, rtg_vec* dstHost, float* timingsMs);
+
 /* ---- persistent context: scene resident in HBM, caller-owned streams ---- */
 typedef struct rtg_context rtg_context;
 int rtg_context_create(int device, rtg_context** out);
@@ -114,6 +128,15 @@ unsigned rtg_shard_global_row(unsigned localRow, unsigned rowBlock, unsigned sha
 int rtg_render_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
                       float aliasFactor, int stackSize, unsigned rowBlock, unsigned shard,
                       unsigned nShards, rtg_vec* dstDevice, void* stream);
+
+/* Restore row order after a gather of row-cyclic shards:
+ * `gathered` holds nShards shard buffers of paddedRows x width rtg_vec each
+ * (shard g's rows as rtg_render_device(..., rowBlock, g, nShards) packs them,
+ * padded to paddedRows = ceil(ceil(H / rowBlock) / nShards) * rowBlock);
+ * writes the height x width frame to `frame` on `stream`.  Device memory. */
+int rtg_assemble_shards_device(rtg_context* ctx, const rtg_vec* gathered, unsigned nShards,
+                               unsigned paddedRows, unsigned width, unsigned height,
+                               unsigned rowBlock, rtg_vec* frame, void* stream);
 
 /* Render an explicit list of global rows (each < height) into dstDevice
  * (nRows * width rtg_vec, in list order); rowsDevice is device memory. */
@@ -170,6 +193,22 @@ void rtg_make_material(float opacity, float glossFactor, const rtg_vec* matte,
  * seed 42 is the benchmark scene. */
 int rtg_scene_generate(unsigned long long seed, unsigned sphNum, unsigned lgtNum,
                        rtg_sphere* spheres, rtg_light* lights);
+
+/* ---- scene files (the reference hard-codes main.cpp:104-168) ----
+ * Text format, one record per line ('#' starts a comment):
+ *   material NAME opacity glossFactor mr mg mb gr gg gb refractiveIndex
+ *   sphere x y z radius NAME
+ *   sphere_raw x y z radius mr mg mb gr gg gb opacity refractiveIndex
+ *   light x y z r g b
+ * `material` builds the record with rtg_make_material (the reference's
+ * setters).  Loads up to sphCap / lgtCap records and sets *sphNum / *lgtNum
+ * to the file's totals (call with capacity 0 to size the arrays).  Errors
+ * name the file and line.  rtg_scene_save writes sphere_raw / light records
+ * that load back bit for bit. */
+int rtg_scene_load(const char* path, rtg_sphere* spheres, unsigned sphCap, unsigned* sphNum,
+                   rtg_light* lights, unsigned lgtCap, unsigned* lgtNum);
+int rtg_scene_save(const char* path, const rtg_sphere* spheres, unsigned sphNum,
+                   const rtg_light* lights, unsigned lgtNum);
 
 #ifdef __cplusplus
 }

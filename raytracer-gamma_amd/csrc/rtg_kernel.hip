@@ -63,6 +63,25 @@ __global__ __launch_bounds__(256) void max_kernel(const float* __restrict__ c, s
   }
 }
 
+// Row-cyclic shards back to row order: grid.y = global row block gb (shard
+// gb % G, local block gb / G), each block of rows is one contiguous copy.
+template <class T>
+__global__ __launch_bounds__(256) void assemble_kernel(const T* __restrict__ gathered,
+                                                       T* __restrict__ frame, unsigned G,
+                                                       unsigned Rmax, unsigned H, unsigned B,
+                                                       size_t rowElems) {
+  const unsigned gb = blockIdx.y;
+  const unsigned g = gb % G, lb = gb / G;
+  const unsigned row0 = gb * B;
+  const unsigned rows = (H - row0 < B) ? (H - row0) : B;
+  const size_t n = (size_t)rows * rowElems;
+  const T* src = gathered + ((size_t)g * Rmax + (size_t)lb * B) * rowElems;
+  T* dst = frame + (size_t)row0 * rowElems;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
 __global__ void max_finish_kernel(unsigned* m) {
   if (__uint_as_float(*m) == 0.f) *m = __float_as_uint(1.f);
 }
@@ -467,6 +486,47 @@ int rtg_max_colour_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t 
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(max_finish_kernel, dim3(1), dim3(1), 0, s, (unsigned*)maxDevice);
+  HIP_TRY(hipGetLastError());
+  return RTG_OK;
+}
+
+int rtg_assemble_shards_device(rtg_context* ctx, const rtg_vec* gathered, unsigned nShards,
+                               unsigned paddedRows, unsigned width, unsigned height,
+                               unsigned rowBlock, rtg_vec* frame, void* stream) {
+  rtg_clear_error();
+  if (!ctx || !gathered || !frame || nShards == 0 || rowBlock == 0 || width == 0 ||
+      height == 0) {
+    rtg_set_error("rtg_assemble_shards_device: invalid arguments");
+    return RTG_ERR_INVALID;
+  }
+  const unsigned nb = (height + rowBlock - 1) / rowBlock;
+  const unsigned need = ((nb + nShards - 1) / nShards) * rowBlock;
+  if (paddedRows < need) {
+    rtg_set_error("rtg_assemble_shards_device: paddedRows %u < %u", paddedRows, need);
+    return RTG_ERR_INVALID;
+  }
+  if (nb > 65535u) {
+    rtg_set_error("rtg_assemble_shards_device: %u row blocks (max 65535)", nb);
+    return RTG_ERR_INVALID;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t rowBytes = (size_t)width * sizeof(rtg_vec);
+  const size_t perBlock = rowBytes * rowBlock;
+  unsigned gx = (unsigned)((perBlock / 16 + 255) / 256);
+  if (gx > 64) gx = 64;
+  if (gx == 0) gx = 1;
+  const dim3 grid(gx, nb);
+  const bool v16 = rowBytes % 16 == 0 && ((uintptr_t)gathered % 16 == 0) &&
+                   ((uintptr_t)frame % 16 == 0);
+  if (v16)
+    hipLaunchKernelGGL(assemble_kernel<uint4>, grid, dim3(256), 0, st,
+                       (const uint4*)gathered, (uint4*)frame, nShards, paddedRows, height,
+                       rowBlock, rowBytes / 16);
+  else
+    hipLaunchKernelGGL(assemble_kernel<unsigned>, grid, dim3(256), 0, st,
+                       (const unsigned*)gathered, (unsigned*)frame, nShards, paddedRows, height,
+                       rowBlock, rowBytes / 4);
   HIP_TRY(hipGetLastError());
   return RTG_OK;
 }

@@ -38,6 +38,9 @@ static void usage() {
   printf("      --seed       S       Scene generator seed (default 42)\n");
   printf("      --out        FILE    Output PPM (default testPPM.ppm)\n");
   printf("      --repeat     K       Render K times, report the best time\n");
+  printf("      --scene      FILE    Load the scene from FILE (format: include/rtg.h)\n");
+  printf("      --save-scene FILE    Write the scene used to FILE\n");
+  printf("      --gpus       N       Render on devices 0..N-1 (row-cyclic shards, RCCL gather)\n");
   printf("\n");
 }
 
@@ -53,7 +56,8 @@ int main(int argc, char** argv) {
   unsigned device = 0, W = 800, H = 600, nSph = 3, nLgt = 2, depth = 5, repeat = 1;
   unsigned long long seed = 42;
   float aa = 3.f, zoom = -4.f;
-  std::string out = "testPPM.ppm";
+  std::string out = "testPPM.ppm", sceneIn, sceneOut;
+  unsigned gpus = 0;
   for (int i = 1; i < argc; ++i) {
     auto need = [&](const char* opt) -> const char* {
       if (++i >= argc) {
@@ -100,6 +104,12 @@ int main(int argc, char** argv) {
       seed = strtoull(need(a), nullptr, 10);
     } else if (!strcmp(a, "--out")) {
       out = need(a);
+    } else if (!strcmp(a, "--scene")) {
+      sceneIn = need(a);
+    } else if (!strcmp(a, "--save-scene")) {
+      sceneOut = need(a);
+    } else if (!strcmp(a, "--gpus")) {
+      if (!parse_uint(need(a), &gpus) || gpus == 0) { printf("Invalid GPU count\n"); return 1; }
     } else {
       printf("Unknown option %s\n", a);
       usage();
@@ -107,10 +117,25 @@ int main(int argc, char** argv) {
     }
   }
 
-  std::vector<rtg_sphere> spheres(nSph);
-  std::vector<rtg_light> lights(nLgt);
-  check(rtg_scene_generate(seed, nSph, nLgt, spheres.data(), lights.data()),
-        "rtg_scene_generate");
+  std::vector<rtg_sphere> spheres;
+  std::vector<rtg_light> lights;
+  if (!sceneIn.empty()) {
+    check(rtg_scene_load(sceneIn.c_str(), nullptr, 0, &nSph, nullptr, 0, &nLgt),
+          "rtg_scene_load");
+    spheres.resize(nSph);
+    lights.resize(nLgt);
+    check(rtg_scene_load(sceneIn.c_str(), spheres.data(), nSph, &nSph, lights.data(), nLgt,
+                         &nLgt),
+          "rtg_scene_load");
+  } else {
+    spheres.resize(nSph);
+    lights.resize(nLgt);
+    check(rtg_scene_generate(seed, nSph, nLgt, spheres.data(), lights.data()),
+          "rtg_scene_generate");
+  }
+  if (!sceneOut.empty())
+    check(rtg_scene_save(sceneOut.c_str(), spheres.data(), nSph, lights.data(), nLgt),
+          "rtg_scene_save");
 
   char info[256];
   check(rtg_device_info((int)device, info, sizeof info), "rtg_device_info");
@@ -120,9 +145,20 @@ int main(int argc, char** argv) {
   double best = 1e30;
   for (unsigned r = 0; r < repeat; ++r) {
     auto t0 = std::chrono::steady_clock::now();
-    check(rtg_render((int)device, spheres.data(), nSph, lights.data(), nLgt, W, H, zoom, aa,
-                     (int)depth + 1, pixels.data()),
-          "rtg_render");
+    if (gpus) {
+      std::vector<int> devs(gpus);
+      for (unsigned g = 0; g < gpus; ++g) devs[g] = (int)g;
+      float tm[3];
+      check(rtg_render_multi(devs.data(), (int)gpus, spheres.data(), nSph, lights.data(), nLgt,
+                             W, H, zoom, aa, (int)depth + 1, 16, pixels.data(), tm),
+            "rtg_render_multi");
+      printf("  %u GPUs: render %.3f ms (slowest device), gather+assemble %.3f ms\n", gpus,
+             (double)tm[0], (double)tm[1]);
+    } else {
+      check(rtg_render((int)device, spheres.data(), nSph, lights.data(), nLgt, W, H, zoom, aa,
+                       (int)depth + 1, pixels.data()),
+            "rtg_render");
+    }
     auto t1 = std::chrono::steady_clock::now();
     double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (ms < best) best = ms;

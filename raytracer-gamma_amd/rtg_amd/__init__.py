@@ -55,7 +55,8 @@ EXPORTED = [
     "rtg_shard_rows", "rtg_shard_global_row", "rtg_render_device", "rtg_render_rows_device",
     "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read", "rtg_diag_timeline",
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
-    "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate",
+    "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate", "rtg_assemble_shards_device",
+    "rtg_render_multi", "rtg_scene_load", "rtg_scene_save",
 ]
 
 
@@ -97,6 +98,11 @@ def lib() -> ctypes.CDLL:
         L.rtg_ppm_bytes.argtypes = [vp, sz, f, vp]
         L.rtg_ppm_bytes.restype = None
         L.rtg_ppm_bytes_device.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.rtg_assemble_shards_device.argtypes = [vp, vp, u, u, u, u, u, vp, vp]
+        L.rtg_render_multi.argtypes = [vp, i, vp, u, vp, u, u, u, f, f, i, u, vp, vp]
+        pu = ctypes.POINTER(u)
+        L.rtg_scene_load.argtypes = [ctypes.c_char_p, vp, u, pu, vp, u, pu]
+        L.rtg_scene_save.argtypes = [ctypes.c_char_p, vp, u, vp, u]
         L.rtg_save_ppm.argtypes = [vp, ctypes.c_char_p, i, i, f]
         L.rtg_make_material.argtypes = [f, f, vp, vp, f, vp]
         L.rtg_make_material.restype = None
@@ -133,6 +139,25 @@ def generate_scene(n_spheres: int, n_lights: int, seed: int = 42):
     _check(lib().rtg_scene_generate(seed, n_spheres, n_lights, _ptr(sph), _ptr(lgt)),
            "rtg_scene_generate")
     return sph, lgt
+
+
+def load_scene_file(path: str):
+    """Spheres and lights of a scene file (rtg_scene_load; format in include/rtg.h)."""
+    n, m = ctypes.c_uint(0), ctypes.c_uint(0)
+    _check(lib().rtg_scene_load(path.encode(), None, 0, ctypes.byref(n), None, 0,
+                                ctypes.byref(m)), "rtg_scene_load")
+    sph = np.zeros(n.value, SPHERE_DTYPE)
+    lgt = np.zeros(m.value, LIGHT_DTYPE)
+    _check(lib().rtg_scene_load(path.encode(), _ptr(sph), n.value, ctypes.byref(n), _ptr(lgt),
+                                m.value, ctypes.byref(m)), "rtg_scene_load")
+    return sph, lgt
+
+
+def save_scene_file(path: str, spheres, lights) -> None:
+    spheres = np.ascontiguousarray(spheres, SPHERE_DTYPE)
+    lights = np.ascontiguousarray(lights, LIGHT_DTYPE)
+    _check(lib().rtg_scene_save(path.encode(), _ptr(spheres), len(spheres), _ptr(lights),
+                                len(lights)), "rtg_scene_save")
 
 
 def reference_scene():
@@ -205,6 +230,23 @@ def render(spheres, lights, width: int, height: int, zoom: float = -4.0,
                             width, height, float(zoom), float(alias_factor), stack_size,
                             _ptr(out)), "rtg_render")
     return out
+
+
+def render_multi(spheres, lights, width: int, height: int, devices=(0,), zoom: float = -4.0,
+                 alias_factor: float = 3.0, stack_size: int = 6, row_block: int = 16):
+    """Multi-GPU one-shot in ONE process (rtg_render_multi): row-cyclic shards on
+    `devices`, one RCCL gather to devices[0].  Returns (frame, timings_ms) with
+    timings = [slowest render, gather + assemble, wall]."""
+    spheres = np.ascontiguousarray(spheres, SPHERE_DTYPE)
+    lights = np.ascontiguousarray(lights, LIGHT_DTYPE)
+    devs = np.ascontiguousarray(devices, np.int32)
+    out = np.empty((height, width, 3), np.float32)
+    tm = np.zeros(3, np.float32)
+    _check(lib().rtg_render_multi(_ptr(devs), len(devs), _ptr(spheres), len(spheres),
+                                  _ptr(lights), len(lights), width, height, float(zoom),
+                                  float(alias_factor), stack_size, row_block, _ptr(out),
+                                  _ptr(tm)), "rtg_render_multi")
+    return out, [float(v) for v in tm]
 
 
 def render_rows(spheres, lights, width: int, height: int, rows, zoom: float = -4.0,
@@ -292,6 +334,16 @@ class Context:
                                            ctypes.c_void_p(dst_ptr),
                                            ctypes.c_void_p(stream) if stream else None),
                "rtg_max_colour_device")
+
+    def assemble_shards_device(self, gathered_ptr: int, n_shards: int, padded_rows: int,
+                               width: int, height: int, row_block: int, frame_ptr: int,
+                               stream: int = 0):
+        """Row order back from gathered row-cyclic shards (rtg_assemble_shards_device)."""
+        _check(lib().rtg_assemble_shards_device(self._h, ctypes.c_void_p(gathered_ptr), n_shards,
+                                                padded_rows, width, height, row_block,
+                                                ctypes.c_void_p(frame_ptr),
+                                                ctypes.c_void_p(stream) if stream else None),
+               "rtg_assemble_shards_device")
 
     def ppm_bytes_device(self, src_ptr: int, n_pixels: int, max_ptr: int, dst_ptr: int,
                          stream: int = 0):

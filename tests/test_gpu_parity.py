@@ -164,6 +164,20 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
         torch.cuda.synchronize()
         fb = dist.assemble(buf, H, B).cpu().numpy()
         assert canon_md5(fb) == c["fb_md5"], G
+        # the native assemble kernel (rtg_assemble_shards_device)
+        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ctx.assemble_shards_device(buf.data_ptr(), G, Rmax, W, H, B, frame.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert canon_md5(frame.cpu().numpy()) == c["fb_md5"], G
+    # odd widths take the 4-byte copy path; 16-byte path for W % 4 == 0
+    for (W2, H2, G, B2) in [(37, 29, 3, 4), (64, 33, 5, 8), (1, 7, 2, 1)]:
+        Rmax = dist.padded_rows(H2, B2, G)
+        buf = torch.randn((G, Rmax, W2, 3), dtype=torch.float32, device="cuda")
+        frame = torch.empty((H2, W2, 3), dtype=torch.float32, device="cuda")
+        ctx.assemble_shards_device(buf.data_ptr(), G, Rmax, W2, H2, B2, frame.data_ptr(), 0)
+        torch.cuda.synchronize()
+        want = dist.assemble(buf.cpu().numpy(), H2, B2)
+        assert np.array_equal(frame.cpu().numpy(), want), (W2, H2, G, B2)
     ctx.close()
 
 
@@ -289,3 +303,21 @@ def test_wave_timeline_diagnostic(R, golden, torch_cuda, variant):
     dur = (rec[:, 1].astype(np.int64) - rec[:, 0].astype(np.int64)) % (1 << 32)
     assert (dur < 100_000_000).all()  # < 1 s each
     ctx.close()
+
+
+def test_render_multi_one_process(R, golden):
+    """rtg_render_multi (one process, RCCL gather over the listed devices) on
+    the devices visible here: bit-identical to the golden frame."""
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    n = R.device_count()
+    devs = list(range(min(n, 8)))
+    for B in (16, 8):
+        fb, tm = R.render_multi(sph, lg, c["W"], c["H"], devices=devs, stack_size=c["stack_size"],
+                                row_block=B)
+        assert canon_md5(fb) == c["fb_md5"], (devs, B)
+        assert tm[0] > 0 and tm[2] >= tm[0]
+    with pytest.raises(R.RtgError):
+        R.render_multi(sph, lg, 8, 8, devices=[0, 0])
+    with pytest.raises(R.RtgError):
+        R.render_multi(sph, lg, 8, 8, devices=[n + 3])

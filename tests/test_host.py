@@ -155,3 +155,71 @@ def test_host_driver_builds_and_prints_help():
     r = subprocess.run([exe, "--help"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0
     assert "--width" in r.stdout and "--device" in r.stdout
+
+
+# ------------------------------------------------------------------ scene files
+def test_reference_scene_file_matches_main_cpp_scene(rtg):
+    """scenes/reference.scene (built with the reference's material setters) is
+    the scene of main.cpp:104-168 bit for bit, i.e. rtg_scene_generate(42, 3, 2)."""
+    sph, lg = rtg.load_scene_file(os.path.join(ROOT, "scenes", "reference.scene"))
+    want_s, want_l = rtg.reference_scene()
+    assert sph.tobytes() == want_s.tobytes()
+    assert lg.tobytes() == want_l.tobytes()
+
+
+@pytest.mark.parametrize("n,m", [(0, 0), (3, 2), (16, 3), (1024, 4)])
+def test_scene_file_round_trip(rtg, tmp_path, n, m):
+    sph, lg = rtg.generate_scene(n, m, 7)
+    rng = np.random.default_rng(n + m)
+    if n:  # awkward floats too: subnormal, negative zero, huge, many digits
+        sph["radius"][0] = np.float32(1.4e-45)
+        sph["pos"][0, 0] = np.float32(-0.0)
+        sph["material"]["opacity"][-1] = np.float32(3.4028235e38)
+        sph["pos"][:, 1] = rng.standard_normal(n).astype(np.float32)
+    path = str(tmp_path / "s.scene")
+    rtg.save_scene_file(path, sph, lg)
+    s2, l2 = rtg.load_scene_file(path)
+    assert s2.tobytes() == sph.tobytes()
+    assert l2.tobytes() == lg.tobytes()
+
+
+def test_scene_file_errors_name_the_line(rtg, tmp_path):
+    cases = {
+        "sphere 1 2 3 4 nosuch\n": "unknown material",
+        "material a 1 0 1 1 1 1 1 1\n": "expected: material",
+        "light 1 2 3 4 5\n": "expected: light",
+        "# ok\nsphere_raw 1 2 3\n": ":2:",
+        "teapot 1 2 3\n": "unknown keyword",
+        "light 1 2 3 4 5 x\n": "expected: light",
+    }
+    for text, msg in cases.items():
+        p = tmp_path / "bad.scene"
+        p.write_text(text)
+        with pytest.raises(rtg.RtgError, match=re.escape(msg)):
+            rtg.load_scene_file(str(p))
+    with pytest.raises(rtg.RtgError, match="I/O error"):
+        rtg.load_scene_file(str(tmp_path / "missing.scene"))
+
+
+def test_scene_file_capacity_query(rtg, tmp_path):
+    """Capacity 0 returns the totals; a short capacity loads a prefix."""
+    sph, lg = rtg.generate_scene(5, 3, 1)
+    path = str(tmp_path / "s.scene")
+    rtg.save_scene_file(path, sph, lg)
+    L = rtg.lib()
+    n, m = ctypes.c_uint(0), ctypes.c_uint(0)
+    assert L.rtg_scene_load(path.encode(), None, 0, ctypes.byref(n), None, 0, ctypes.byref(m)) == 0
+    assert (n.value, m.value) == (5, 3)
+    part = np.zeros(2, rtg.SPHERE_DTYPE)
+    assert L.rtg_scene_load(path.encode(), ctypes.c_void_p(part.ctypes.data), 2, ctypes.byref(n),
+                            None, 0, ctypes.byref(m)) == 0
+    assert n.value == 5 and part.tobytes() == sph[:2].tobytes()
+
+
+def test_host_driver_scene_options(tmp_path):
+    """rtg_main --save-scene / --help (no GPU needed for these)."""
+    exe = os.path.join(PKG, "rtg_main")
+    if not os.path.exists(exe):
+        pytest.skip("rtg_main not built")
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True)
+    assert "--scene" in r.stdout and "--gpus" in r.stdout
