@@ -321,3 +321,18 @@ def test_render_multi_one_process(R, golden):
         R.render_multi(sph, lg, 8, 8, devices=[0, 0])
     with pytest.raises(R.RtgError):
         R.render_multi(sph, lg, 8, 8, devices=[n + 3])
+
+
+@pytest.mark.parametrize("extra", [[], ["--gpus", "1"]])
+def test_host_driver_scene_file_ppm(R, golden, tmp_path, extra):
+    """The C++ host driver (the reference's main() flow) on the reference scene
+    file writes the reference's PPM byte for byte, single- or multi-GPU path."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "raytracer-gamma_amd", "rtg_main")
+    scene = os.path.join(root, "scenes", "reference.scene")
+    out = str(tmp_path / "o.ppm")
+    r = subprocess.run([exe, "--scene", scene, "--out", out] + extra, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert md5(open(out, "rb").read()) == golden["configs"]["ref800"]["ppm_md5"]
