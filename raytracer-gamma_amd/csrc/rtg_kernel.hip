@@ -310,12 +310,13 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   if (rc) return rc;
   int variant = ctx->opts.variant;
   // sample-parallel kernels need all of a pixel's samples in one wave
-  auto isSample = [](int v) { return v == 0 || (v >= 14 && v <= 18) || v == 110; };
+  auto isSample = [](int v) { return v == 0 || (v >= 14 && v <= 19) || v == 110; };
   if (isSample(variant) && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = variant == 110 ? 100 : 9;
   const bool sampleKernel = isSample(variant);
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
-  if (variant == 0 || variant == 15 || variant == 18 || variant == 110) ldsMats = false;
+  if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 110)
+    ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {
     rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);

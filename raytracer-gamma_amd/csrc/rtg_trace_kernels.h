@@ -328,7 +328,7 @@ void trace_kernel(const KernelArgs a) {
 // Requires nAA^2 <= 64; the host launches the default kernel otherwise.
 // Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
 // rows, all their samples) traced by one wave, entered converged.
-template <int S, int Q, bool kDiag, class Sc>
+template <int S, int Q, bool kDiag, class Sc, bool kShfl = false>
 __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
@@ -357,13 +357,32 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   uint64_t primSel = ~0ull;
   bool usePrim = false;
   if (a.n <= 64) {
-    float x0 = valid ? rx : 3.0e38f, x1 = valid ? rx : -3.0e38f;
-    float y0 = valid ? ry : 3.0e38f, y1 = valid ? ry : -3.0e38f;
-    for (int off = 32; off > 0; off >>= 1) {
-      x0 = fminf(x0, __shfl_xor(x0, off));
-      x1 = fmaxf(x1, __shfl_xor(x1, off));
-      y0 = fminf(y0, __shfl_xor(y0, off));
-      y1 = fmaxf(y1, __shfl_xor(y1, off));
+    float x0, x1, y0, y1;
+    // Wave-uniform: do the wave's valid pixels lie in one row?  Then the
+    // bounds are four lanes' values, since every float step of main.cpp:
+    // 419-426 is monotone: rx grows with x and j (lane 0 has the smallest,
+    // the last pixel's j = nAA-1 lane the largest) and ry with i (lane 0, and
+    // lane nAA(nAA-1)).  Otherwise reduce across the wave.
+    const size_t p0 = gw * PPW;
+    const unsigned nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);  // >= 1
+    const bool oneRow = (p0 / a.W) == ((p0 + nv - 1) / a.W);
+    if (oneRow && !kShfl) {
+      x0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rx), 0));
+      x1 = __int_as_float(
+          __builtin_amdgcn_readlane(__float_as_int(rx), (int)((nv - 1) * SP + nAA - 1)));
+      y0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry), 0));
+      y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ry), (int)((nAA - 1) * nAA)));
+    } else {
+      x0 = valid ? rx : 3.0e38f;
+      x1 = valid ? rx : -3.0e38f;
+      y0 = valid ? ry : 3.0e38f;
+      y1 = valid ? ry : -3.0e38f;
+      for (int off = 32; off > 0; off >>= 1) {
+        x0 = fminf(x0, __shfl_xor(x0, off));
+        x1 = fmaxf(x1, __shfl_xor(x1, off));
+        y0 = fminf(y0, __shfl_xor(y0, off));
+        y1 = fmaxf(y1, __shfl_xor(y1, off));
+      }
     }
     bool possible = false;
     if (lane < a.n) {
@@ -389,14 +408,34 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
     if ((threadIdx.x & 63u) == 0)
       for (int k = 0; k < kProbeSlots; ++k) atomicAdd(&a.diag[k], sc.acc[k]);
   }
-  // Ordered per-pixel sum (whole wave converged again).
+  // Ordered per-pixel sum (whole wave converged again): every lane parks its
+  // sample in its own level-0 frame slot (LDS, free again: the trace is done)
+  // and each pixel's first lane reads its nAA^2 samples back in order.
   const unsigned base = pl * SP;
   V3 pix = v3(0.f, 0.f, 0.f);
-  for (unsigned k = 0; k < SP; ++k) {
-    const int src = (int)((base + k) & 63u);
-    pix.x = pix.x + __shfl(c.x, src);
-    pix.y = pix.y + __shfl(c.y, src);
-    pix.z = pix.z + __shfl(c.z, src);
+  if constexpr (kShfl) {  // variant 19: cross-lane reads instead of LDS
+    for (unsigned k = 0; k < SP; ++k) {
+      const int src = (int)((base + k) & 63u);
+      pix.x = pix.x + __shfl(c.x, src);
+      pix.y = pix.y + __shfl(c.y, src);
+      pix.z = pix.z + __shfl(c.z, src);
+    }
+  } else {
+    FrameC* slot0 = sc.lfr - (threadIdx.x & 63u);  // this wave's level-0 slots
+    sc.lfr->cx = c.x;
+    sc.lfr->cy = c.y;
+    sc.lfr->cz = c.z;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (s == 0) {
+      for (unsigned k = 0; k < SP; ++k) {
+        const FrameC& f = slot0[(base + k) & 63u];
+        pix.x = pix.x + f.cx;
+        pix.y = pix.y + f.cy;
+        pix.z = pix.z + f.cz;
+      }
+    }
   }
   if (valid && s == 0) {
     float* o = a.dst + ((size_t)lr * a.W + x) * 3;
@@ -423,7 +462,8 @@ void trace_samples_kernel(const KernelArgs a) {
   stage_scene<S, kLds, kThreads>(a, sc);
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screen every sphere)
-  trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100)>(a, sc, gw);
+  trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19)>(
+      a, sc, gw);
   record_wave(a, t0, gw);
 }
 
@@ -445,6 +485,7 @@ void trace_samples_kernel(const KernelArgs a) {
 //   14 as 0 with four-wave workgroups
 //   15 as 0 with shadow rays screening every sphere (no shadow masks)
 //   18 as 0 built for 8 waves per SIMD (<= 64 VGPRs)
+//   19 as 0 with shuffle reductions for the cull bounds and the pixel sum
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
 //    pixel groups, were removed: register spills made them slower)
 //   16 as 17 with two-wave workgroups
@@ -456,7 +497,7 @@ template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15 || V == 18 || V == 110)
+  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 110)
     return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -467,6 +508,7 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 100: return trace_fn_v<S, 100>(lds);
     case 110: return trace_fn_v<S, 110>(lds);
     case 18: return trace_fn_v<S, 18>(lds);
+    case 19: return trace_fn_v<S, 19>(lds);
     case 104: return trace_fn_v<S, 104>(lds);
     case 1: return trace_fn_v<S, 1>(lds);
     case 4: return trace_fn_v<S, 4>(lds);

@@ -261,7 +261,7 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 100, 108, 110])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 19, 100, 108, 110])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda
