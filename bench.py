@@ -200,7 +200,7 @@ def main():
                               n_shards=1, stream=sptr)
             if i is not None:
                 ev_k[i][1].record(stream)
-            frame = shard
+            frame = shard[:H]
             return
         works = []
         for c in range(K):
