@@ -149,6 +149,17 @@ int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
                     float zoom, float aliasFactor, int stackSize, const unsigned* rows,
                     unsigned nRows, rtg_vec* dstHost);
 
+/* Semantics of a context's renders.  RTG_SEMANTICS_CPU (default) is the
+ * reference CPU path (raytracer.h), bit for bit.  RTG_SEMANTICS_OPENCL is the
+ * reference's OpenCL kernel (raytrace_kernel.cl:641-867) under IEEE binary32:
+ * f32 Fresnel (:399-432) and sinA1 (:507), the return register zeroed by the
+ * reflection push (:835-845); pass stackSize 5 for the .cl's RTSTACK_MAXSIZE
+ * (:58).  That kernel ran under OpenCL's relaxed division/sqrt, so its own
+ * output (testPPM.ppm) is only approached, not reproduced bit for bit. */
+#define RTG_SEMANTICS_CPU 0
+#define RTG_SEMANTICS_OPENCL 1
+int rtg_context_set_semantics(rtg_context* ctx, int semantics);
+
 /* Launch-configuration knobs (performance only; results never change). */
 typedef struct rtg_launch_opts {
   int variant;        /* 0 = default kernel; other values select A/B variants */

@@ -148,11 +148,21 @@ static OVec calculateMatte(const OSph* sph, unsigned n, const OLight* lg, unsign
   return sum;
 }
 
-/* raytracer.h:370-403 — note the double-precision island. */
-static float polarisedReflection(float n1, float n2, float cosA1, float cosA2) {
+/* raytracer.h:370-403 — note the double-precision island.  cl: the OpenCL
+ * kernel's all-float version, raytrace_kernel.cl:399-432. */
+static float polarisedReflection(float n1, float n2, float cosA1, float cosA2, int cl) {
   const float kEPSILON = 1.0e-6f;
   const float left = n1 * cosA1;
   const float right = n2 * cosA2;
+  if (cl) {
+    const float numerator = left - right;
+    float denominator = left + right;
+    denominator *= denominator;
+    if (denominator < kEPSILON) return 1.f;
+    float reflection = (numerator * numerator) / denominator;
+    if (reflection > 1.f) reflection = 1.f;
+    return reflection;
+  }
   double numerator = left - right;     /* float subtract, then widen */
   double denominator = left + right;   /* float add, then widen */
   denominator *= denominator;
@@ -196,11 +206,13 @@ static OMat bgMaterial(void) {
 
 /* raytracer.h:642-815 */
 static ORay calculateRefraction(const OSph* sph, unsigned n, const OIsect* is, ORay inc,
-                                const OMat* refrMat, OMat* tgt, float* outR, OCount* cnt) {
+                                const OMat* refrMat, OMat* tgt, float* outR, OCount* cnt,
+                                int cl) {
   float cosA1 = vdot(inc.dir, is->normal);
   float sinA1 = 0.f;
   if (cosA1 <= -1.0) { cosA1 = -1.f; sinA1 = 0.f; }
   else if (cosA1 >= +1.f) { cosA1 = 1.f; sinA1 = 0.f; }
+  else if (cl) { sinA1 = sqrtf(1.f - (cosA1 * cosA1)); }          /* raytrace_kernel.cl:507 */
   else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }  /* :683, f64 sqrt */
 
   const float kSmallShift = 0.01f;
@@ -225,9 +237,9 @@ static ORay calculateRefraction(const OSph* sph, unsigned n, const OIsect* is, O
   }
   float cosA2 = sqrtf(1.f - (sinA2 * sinA2));                     /* :776, f32 sqrt */
   if (cosA1 < 0.f) cosA2 = -cosA2;
-  const float Rs = polarisedReflection(refrMat->refr, tgt->refr, cosA1, cosA2);
-  const float Rp = polarisedReflection(refrMat->refr, tgt->refr, cosA2, cosA1);
-  *outR = (float)((double)(Rs + Rp) * 0.5);                       /* :798 */
+  const float Rs = polarisedReflection(refrMat->refr, tgt->refr, cosA1, cosA2, cl);
+  const float Rp = polarisedReflection(refrMat->refr, tgt->refr, cosA2, cosA1, cl);
+  *outR = (float)((double)(Rs + Rp) * 0.5);                       /* :798 (exact either way) */
 
   ORay out;
   out.intensity = vsmul((1.f - *outR), inc.intensity);            /* :807 */
@@ -266,7 +278,7 @@ static void stPush(OStack* s, const OSnap* e) {
 
 /* raytracer.h:410-636 */
 static OVec rayTrace(const OSph* sph, unsigned n, const OLight* lg, unsigned m, ORay ray,
-                     OMat refrMat, int traceDepth, int S, OCount* cnt) {
+                     OMat refrMat, int traceDepth, int S, OCount* cnt, int cl) {
   const int kMaxTraceDepth = 0x7FFFFFFF - 1;  /* RSIZE_MAX - 1 (Win32 value) */
   OVec colourSum = v3(0.f, 0.f, 0.f);
   OStack st;
@@ -305,7 +317,7 @@ static OVec rayTrace(const OSph* sph, unsigned n, const OLight* lg, unsigned m, 
                 rr.origin = cur.ray.origin;
                 OMat tgt;
                 ORay refracted = calculateRefraction(sph, n, &cur.isect, rr, &cur.refrMat,
-                                                     &tgt, &R, cnt);
+                                                     &tgt, &R, cnt, cl);
                 cur.R = R;
                 cur.stage = 1;
                 stPush(&st, &cur);
@@ -351,6 +363,9 @@ static OVec rayTrace(const OSph* sph, unsigned n, const OLight* lg, unsigned m, 
           ns.colour = v3(0.f, 0.f, 0.f);
           ns.refrMat = cur.refrMat;
           stPush(&st, &ns);
+          /* raytrace_kernel.cl:835-845 reuses currSnapshot as the child (colour
+           * 0) before `colourSum = currSnapshot.colour` */
+          if (cl) { colourSum = ns.colour; break; }
         }
         colourSum = cur.colour;
         break;
@@ -368,7 +383,7 @@ static OVec rayTrace(const OSph* sph, unsigned n, const OLight* lg, unsigned m, 
 /* main.cpp:411-452 (commented-out CPU loop). */
 static void shadePixel(const OSph* sph, unsigned n, const OLight* lg, unsigned m, unsigned W,
                        unsigned H, float zoom, float aa, int S, unsigned gid, float* dst,
-                       OCount* cnt) {
+                       OCount* cnt, int cl) {
   const float xs = 16.f / ((float)W);
   const float ys = 12.f / ((float)H);
   const float asp = 16.f / 12.f;
@@ -387,7 +402,7 @@ static void shadePixel(const OSph* sph, unsigned n, const OLight* lg, unsigned m
       float x = (pxX + (float)(((float)j) * st)) * asp;
       float y = (pxY + (float)(((float)i) * st));
       ray.dir = vnorm(v3(x, y, zoom));
-      OVec c = rayTrace(sph, n, lg, m, ray, bg, 0, S, cnt);
+      OVec c = rayTrace(sph, n, lg, m, ray, bg, 0, S, cnt, cl);
       c = vsmul(inv, c);
       pix = vadd(pix, c);
     }
@@ -399,7 +414,7 @@ static void shadePixel(const OSph* sph, unsigned n, const OLight* lg, unsigned m
 
 typedef struct {
   const OSph* sph; unsigned n; const OLight* lg; unsigned m;
-  unsigned W, H; float zoom, aa; int S;
+  unsigned W, H; float zoom, aa; int S, cl;
   const unsigned* rows; unsigned nrows; float* out;
   volatile unsigned next; pthread_mutex_t mu;
   OCount total;
@@ -416,7 +431,7 @@ static void* worker(void* p) {
     unsigned y = j->rows[k];
     for (unsigned x = 0; x < j->W; ++x)
       shadePixel(j->sph, j->n, j->lg, j->m, j->W, j->H, j->zoom, j->aa, j->S, y * j->W + x,
-                 j->out + ((size_t)k * j->W + x) * 3, &c);
+                 j->out + ((size_t)k * j->W + x) * 3, &c, j->cl);
   }
   pthread_mutex_lock(&j->mu);
   j->total.sphere_tests += c.sphere_tests;
@@ -426,13 +441,14 @@ static void* worker(void* p) {
   return 0;
 }
 
-int oracle_render_rows(const void* spheres, unsigned n, const void* lights, unsigned m,
+static int render_rows(const void* spheres, unsigned n, const void* lights, unsigned m,
                        unsigned W, unsigned H, float zoom, float aliasFactor, int stackSize,
                        const unsigned* rows, unsigned nrows, float* out, int nthreads,
-                       unsigned long long* counters) {
+                       unsigned long long* counters, int cl) {
   if (stackSize < 1 || stackSize > ORACLE_MAX_STACK) return -1;
   Job j;
   memset(&j, 0, sizeof j);
+  j.cl = cl;
   j.sph = (const OSph*)spheres; j.n = n; j.lg = (const OLight*)lights; j.m = m;
   j.W = W; j.H = H; j.zoom = zoom; j.aa = aliasFactor; j.S = stackSize;
   j.rows = rows; j.nrows = nrows; j.out = out;
@@ -453,6 +469,26 @@ int oracle_render_rows(const void* spheres, unsigned n, const void* lights, unsi
     counters[2] = j.total.contain_tests;
   }
   return 0;
+}
+
+int oracle_render_rows(const void* spheres, unsigned n, const void* lights, unsigned m,
+                       unsigned W, unsigned H, float zoom, float aliasFactor, int stackSize,
+                       const unsigned* rows, unsigned nrows, float* out, int nthreads,
+                       unsigned long long* counters) {
+  return render_rows(spheres, n, lights, m, W, H, zoom, aliasFactor, stackSize, rows, nrows,
+                     out, nthreads, counters, 0);
+}
+
+/* The semantics of the reference's OpenCL kernel (raytrace_kernel.cl) under
+ * IEEE binary32 arithmetic: f32 Fresnel (:399-432) and f32 sinA1 (:507), and
+ * the return register zeroed by the reflection push (:835-845); the stack
+ * capacity is the caller's (5 in the .cl, :58).  NOT pinned bit for bit: the
+ * .cl ran under OpenCL's relaxed division/sqrt and FP contraction. */
+int oracle_render_rows_cl(const void* spheres, unsigned n, const void* lights, unsigned m,
+                          unsigned W, unsigned H, float zoom, float aliasFactor, int stackSize,
+                          const unsigned* rows, unsigned nrows, float* out, int nthreads) {
+  return render_rows(spheres, n, lights, m, W, H, zoom, aliasFactor, stackSize, rows, nrows,
+                     out, nthreads, 0, 1);
 }
 
 /* algebra.h:68-91 */

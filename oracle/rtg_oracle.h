@@ -15,6 +15,11 @@ int oracle_render_rows(const void* spheres, unsigned n, const void* lights, unsi
                        const unsigned* rows, unsigned nrows, float* out, int nthreads,
                        unsigned long long* counters);
 
+/* Same, with the OpenCL kernel's semantics (raytrace_kernel.cl; see the .c). */
+int oracle_render_rows_cl(const void* spheres, unsigned n, const void* lights, unsigned m,
+                          unsigned W, unsigned H, float zoom, float aliasFactor, int stackSize,
+                          const unsigned* rows, unsigned nrows, float* out, int nthreads);
+
 /* algebra.h:68-91 maxColourValuePixelBuffer. */
 float oracle_max_colour(const float* fb, unsigned long long npx);
 

@@ -121,6 +121,7 @@ struct rtg_context {
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
   size_t timelineCap = 0, timelineCount = 0;
   rtg_launch_opts opts{};
+  int semantics = RTG_SEMANTICS_CPU;
   bool hasScene = false;
 };
 
@@ -242,6 +243,16 @@ int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* coun
   return RTG_OK;
 }
 
+int rtg_context_set_semantics(rtg_context* ctx, int semantics) {
+  rtg_clear_error();
+  if (!ctx || (semantics != RTG_SEMANTICS_CPU && semantics != RTG_SEMANTICS_OPENCL)) {
+    rtg_set_error("rtg_context_set_semantics: invalid arguments");
+    return RTG_ERR_INVALID;
+  }
+  ctx->semantics = semantics;
+  return RTG_OK;
+}
+
 int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts) {
   rtg_clear_error();
   if (!ctx || !opts) return RTG_ERR_INVALID;
@@ -310,12 +321,15 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   if (rc) return rc;
   int variant = ctx->opts.variant;
   // sample-parallel kernels need all of a pixel's samples in one wave
-  auto isSample = [](int v) { return v == 0 || (v >= 14 && v <= 19) || v == 110; };
-  if (isSample(variant) && (a.cam.nAA < 1 || a.cam.nAA > 8)) variant = variant == 110 ? 100 : 9;
+  if (ctx->semantics == RTG_SEMANTICS_OPENCL) variant = 50;  // results differ: not a knob
+  auto isSample = [](int v) { return v == 0 || (v >= 14 && v <= 19) || v == 50 || v == 110; };
+  if (isSample(variant) && (a.cam.nAA < 1 || a.cam.nAA > 8))
+    variant = variant == 110 ? 100 : variant == 50 ? 59 : 9;
   const bool sampleKernel = isSample(variant);
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
-  if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 110)
+  if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 50 ||
+      variant == 110)
     ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {

@@ -277,10 +277,21 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
   return sum;
 }
 
-// raytracer.h:370-403 (f64 island).
+// raytracer.h:370-403 (f64 island).  kCL: the OpenCL kernel's all-float
+// version, raytrace_kernel.cl:399-432.
+template <bool kCL = false>
 RTG_HD float polarised_reflection(float n1, float n2, float cosA1, float cosA2) {
   const float left = n1 * cosA1;
   const float right = n2 * cosA2;
+  if constexpr (kCL) {
+    const float num = left - right;
+    float den = left + right;
+    den *= den;
+    if (den < 1.0e-6f) return 1.f;
+    float refl = (num * num) / den;
+    if (refl > 1.f) refl = 1.f;
+    return refl;
+  }
   const double num = (double)(left - right);
   double den = (double)(left + right);
   den *= den;
@@ -292,13 +303,14 @@ RTG_HD float polarised_reflection(float n1, float n2, float cosA1, float cosA2) 
 
 // raytracer.h:642-815.  Computes the reflection factor R and, when wantRay,
 // the refracted direction.  Returns the target material index.
-template <class Scene>
+template <bool kCL = false, class Scene>
 RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRay,
                       V3& dirOut, float& R) {
   float cosA1 = vdot(D, N);
   float sinA1 = 0.f;
   if (cosA1 <= -1.0f) { cosA1 = -1.f; sinA1 = 0.f; }
   else if (cosA1 >= 1.f) { cosA1 = 1.f; sinA1 = 0.f; }
+  else if (kCL) { sinA1 = rtg_sqrtf(1.f - (cosA1 * cosA1)); }  // raytrace_kernel.cl:507
   else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }
 
   const V3 testPt = vadd(vsmul(0.01f, D), P);
@@ -342,15 +354,19 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   }
   float cosA2 = rtg_sqrtf(1.f - (sinA2 * sinA2));
   if (cosA1 < 0.f) cosA2 = -cosA2;
-  const float Rs = polarised_reflection(nSrc, nTgt, cosA1, cosA2);
-  const float Rp = polarised_reflection(nSrc, nTgt, cosA2, cosA1);
+  const float Rs = polarised_reflection<kCL>(nSrc, nTgt, cosA1, cosA2);
+  const float Rp = polarised_reflection<kCL>(nSrc, nTgt, cosA2, cosA1);
   R = (float)((double)(Rs + Rp) * 0.5);
   return tgt;
 }
 
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
-template <int S, int Q, class Scene, class FStore>
+// kCL: the reference OpenCL kernel's semantics (raytrace_kernel.cl:641-867):
+// f32 Fresnel and sinA1, and the return register zeroed by the reflection
+// push (:835-845), so a reflection child that leaves it stale returns 0 and a
+// leaf's colour is doubled once, not twice.
+template <int S, int Q, bool kCL = false, class Scene, class FStore>
 RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = false,
                        uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
@@ -410,7 +426,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         V3 cdir;
         float R;
         sc.probe_begin(kProbeRefraction);
-        const int tgt = refraction(sc, d, P, N, mr.refr, !leaf, cdir, R);
+        const int tgt = refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R);
         sc.probe_end(kProbeRefraction);
         // stage-1 reflection colour, raytracer.h:563-578
         const float prod = tr * R;
@@ -447,7 +463,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         }
         // Leaf: both children dropped by the full stack.
         const V3 c1 = vadd(colour, colour);
-        ret = sigR ? vadd(c1, c1) : c1;
+        ret = (sigR && !kCL) ? vadd(c1, c1) : c1;
       } else {
         ret = colour;
       }
@@ -467,6 +483,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
         o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 2);
+        if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
         descend = true;
         break;
       }
@@ -1304,7 +1321,7 @@ RTG_HD V3 sample_dir(const Camera& cam, unsigned x, unsigned y, int i, int j, fl
 }
 
 // main.cpp:411-452 for pixel (x, y) of the frame.
-template <int S, int Q, bool kSceneFrames = false, class Scene>
+template <int S, int Q, bool kSceneFrames = false, bool kCL = false, class Scene>
 RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y,
                       bool usePrim = false, uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
@@ -1318,8 +1335,9 @@ RTG_HD V3 shade_pixel(const Scene& sc, const Camera& cam, unsigned x, unsigned y
       const float ry = (pxY + (float)(((float)i) * cam.st));
       const V3 dir = vnorm(v3(rx, ry, cam.zoom));
       V3 c;
-      if constexpr (kSceneFrames) c = trace_sample<S, Q>(sc, dir, sc.frames(), usePrim, primSel);
-      else c = trace_sample<S, Q>(sc, dir, local, usePrim, primSel);
+      if constexpr (kSceneFrames)
+        c = trace_sample<S, Q, kCL>(sc, dir, sc.frames(), usePrim, primSel);
+      else c = trace_sample<S, Q, kCL>(sc, dir, local, usePrim, primSel);
       c = vsmul(cam.inv, c);
       pix = vadd(pix, c);
     }

@@ -238,7 +238,7 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
   // per lane against that bundle, then a ballot (see primary_sphere_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if constexpr (kBase == 0 || kBase == 8 || kBase == 9) {
+  if constexpr (kBase == 0 || kBase == 8 || kBase == 9 || kBase == 59) {
     if (a.n <= 64) {
       float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
       if (valid) primary_bounds(a.cam, x, gy, x0, x1, y0, y1);
@@ -267,6 +267,8 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
   }
   if constexpr (kBase == 0 || kBase == 9)
     pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy, usePrim, primSel);
+  else if constexpr (kBase == 59)  // OpenCL semantics (rtg_context_set_semantics)
+    pix = shade_pixel<S, 2, true, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 6) pix = shade_pixel<S, 2, true>(sc, a.cam, x, gy);
   else if constexpr (kBase == 8) pix = shade_pixel<S, 3, true>(sc, a.cam, x, gy, usePrim, primSel);
   else if constexpr (kBase == 5) pix = shade_pixel<S, 2, false>(sc, a.cam, x, gy);
@@ -328,7 +330,7 @@ void trace_kernel(const KernelArgs a) {
 // Requires nAA^2 <= 64; the host launches the default kernel otherwise.
 // Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
 // rows, all their samples) traced by one wave, entered converged.
-template <int S, int Q, bool kDiag, class Sc, bool kShfl = false>
+template <int S, int Q, bool kDiag, class Sc, bool kShfl = false, bool kCL = false>
 __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
@@ -400,7 +402,7 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
     tk0 = __builtin_amdgcn_s_memtime();
   }
   if (valid) {
-    c = trace_sample<S, Q>(sc, dir, sc.frames(), usePrim, primSel);
+    c = trace_sample<S, Q, kCL>(sc, dir, sc.frames(), usePrim, primSel);
     c = vsmul(a.cam.inv, c);
   }
   if constexpr (kDiag) {  // wave converged again: one add per slot
@@ -462,8 +464,8 @@ void trace_samples_kernel(const KernelArgs a) {
   stage_scene<S, kLds, kThreads>(a, sc);
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screen every sphere)
-  trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19)>(
-      a, sc, gw);
+  trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
+              (kVariant == 50)>(a, sc, gw);
   record_wave(a, t0, gw);
 }
 
@@ -486,6 +488,8 @@ void trace_samples_kernel(const KernelArgs a) {
 //   15 as 0 with shadow rays screening every sphere (no shadow masks)
 //   18 as 0 built for 8 waves per SIMD (<= 64 VGPRs)
 //   19 as 0 with shuffle reductions for the cull bounds and the pixel sum
+//   50 / 59: 0 / 9 with the OpenCL kernel's semantics (RTG_SEMANTICS_OPENCL;
+//     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
 //    pixel groups, were removed: register spills made them slower)
 //   16 as 17 with two-wave workgroups
@@ -497,7 +501,7 @@ template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 110)
+  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 50 || V == 110)
     return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -509,6 +513,8 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 110: return trace_fn_v<S, 110>(lds);
     case 18: return trace_fn_v<S, 18>(lds);
     case 19: return trace_fn_v<S, 19>(lds);
+    case 50: return trace_fn_v<S, 50>(lds);
+    case 59: return trace_fn_v<S, 59>(lds);
     case 104: return trace_fn_v<S, 104>(lds);
     case 1: return trace_fn_v<S, 1>(lds);
     case 4: return trace_fn_v<S, 4>(lds);

@@ -56,7 +56,7 @@ EXPORTED = [
     "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read", "rtg_diag_timeline",
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate", "rtg_assemble_shards_device",
-    "rtg_render_multi", "rtg_scene_load", "rtg_scene_save",
+    "rtg_render_multi", "rtg_scene_load", "rtg_scene_save", "rtg_context_set_semantics",
 ]
 
 
@@ -90,6 +90,7 @@ def lib() -> ctypes.CDLL:
         L.rtg_render_rows_device.argtypes = [vp, u, u, f, f, i, vp, u, vp, vp]
         L.rtg_render_rows.argtypes = [i, vp, u, vp, u, u, u, f, f, i, vp, u, vp]
         L.rtg_set_launch_opts.argtypes = [vp, vp]
+        L.rtg_context_set_semantics.argtypes = [vp, i]
         L.rtg_diag_read.argtypes = [vp, vp, i]
         L.rtg_diag_timeline.argtypes = [vp, vp, sz, vp]
         L.rtg_max_colour.argtypes = [vp, sz]
@@ -291,6 +292,12 @@ class Context:
                "rtg_context_set_scene")
 
     LAUNCH_TIMELINE = 1  # RTG_LAUNCH_TIMELINE
+    SEMANTICS_CPU, SEMANTICS_OPENCL = 0, 1  # RTG_SEMANTICS_*
+
+    def set_semantics(self, semantics: int):
+        """CPU path (default, bit-exact) or the reference OpenCL kernel's semantics."""
+        _check(lib().rtg_context_set_semantics(self._h, int(semantics)),
+               "rtg_context_set_semantics")
 
     def set_variant(self, variant: int, flags: int = 0):
         opts = (ctypes.c_int * 8)(variant, flags, 0, 0, 0, 0, 0, 0)

@@ -67,6 +67,17 @@ class Oracle:
         self.counters = [int(c) for c in cnt]
         return out
 
+    def render_cl(self, sph, lg, W, H, S, rows=None, aa=3.0, zoom=-4.0, threads=None):
+        """The reference OpenCL kernel's semantics (oracle_render_rows_cl)."""
+        rows = np.arange(H, dtype=np.uint32) if rows is None else np.asarray(rows, np.uint32)
+        out = np.zeros((len(rows), W, 3), np.float32)
+        threads = threads or min(16, os.cpu_count() or 1)
+        rc = self.lib.oracle_render_rows_cl(P(sph), len(sph), P(lg), len(lg), W, H,
+                                            ctypes.c_float(zoom), ctypes.c_float(aa), S, P(rows),
+                                            len(rows), P(out), threads)
+        assert rc == 0
+        return out
+
     def max_colour(self, fb):
         fb = np.ascontiguousarray(fb, np.float32)
         return self.lib.oracle_max_colour(P(fb), fb.size // 3)

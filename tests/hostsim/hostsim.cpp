@@ -92,13 +92,15 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 8: p = rtg::shade_pixel<S, 3, true>(sc, cam, x, y); break;
       case 0:
       case 14:
-      case 15: {  // sample-parallel kernel: samples traced one by one, summed in order
+      case 15:
+      case 50: {  // sample-parallel kernel: samples traced one by one, summed in order
         p = rtg::v3(0.f, 0.f, 0.f);
         for (int s = 0; s < cam.nAA * cam.nAA; ++s) {
           float rx, ry;
           const rtg::V3 d = rtg::sample_dir(cam, x, y, s / cam.nAA, s % cam.nAA, rx, ry);
-          rtg::V3 c = g_variant == 15 ? rtg::trace_sample<S, 2>(sc, d, sc.frames())
-                                      : rtg::trace_sample<S, 4>(sc, d, sc.frames());
+          rtg::V3 c = g_variant == 15   ? rtg::trace_sample<S, 2>(sc, d, sc.frames())
+                      : g_variant == 50 ? rtg::trace_sample<S, 4, true>(sc, d, sc.frames())
+                                        : rtg::trace_sample<S, 4>(sc, d, sc.frames());
           c = rtg::vsmul(cam.inv, c);
           p = rtg::vadd(p, c);
         }

@@ -336,3 +336,46 @@ def test_host_driver_scene_file_ppm(R, golden, tmp_path, extra):
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert md5(open(out, "rb").read()) == golden["configs"]["ref800"]["ppm_md5"]
+
+
+def test_opencl_semantics_vs_oracle(R, oracle, torch_cuda):
+    """rtg_context_set_semantics(RTG_SEMANTICS_OPENCL): the reference OpenCL
+    kernel's semantics, bit-exact against the OpenCL-semantics oracle, through
+    the sample kernel and its nAA > 8 fallback."""
+    torch = torch_cuda
+    ctx = R.Context(0)
+    ctx.set_semantics(ctx.SEMANTICS_OPENCL)
+    rng = np.random.default_rng(2027)
+    cases = [(5, 3.0, -4.0, None)] + [None] * 14
+    for trial, case in enumerate(cases):
+        if case is None:
+            S = int(rng.integers(1, 17))
+            aa = float(rng.choice([1.0, 2.0, 3.0, 9.0]))
+            zoom = float(rng.choice([-4.0, 3.0]))
+            n, m = int(rng.integers(0, 20)), int(rng.integers(0, 5))
+            sph, lg = random_scene(rng, n, m)
+            if zoom > 0:
+                sph["pos"][:, 2] *= -1.0
+            W, H = int(rng.integers(1, 60)), int(rng.integers(1, 40))
+        else:
+            S, aa, zoom, _ = case
+            sph, lg = R.reference_scene()
+            W, H = 160, 120
+        want = oracle.render_cl(sph, lg, W, H, S, aa=aa, zoom=zoom)
+        ctx.set_scene(sph, lg)
+        out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ctx.render_device(W, H, out.data_ptr(), zoom=zoom, alias_factor=aa, stack_size=S,
+                          stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert bits_equal(got, want), (trial, S, W, H, aa, first_mismatch(got, want))
+    ctx.set_semantics(ctx.SEMANTICS_CPU)
+    sph, lg = R.reference_scene()
+    ctx.set_scene(sph, lg)
+    out = torch.empty((60, 80, 3), dtype=torch.float32, device="cuda")
+    ctx.render_device(80, 60, out.data_ptr(), stack_size=5)
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), oracle.render(sph, lg, 80, 60, 5))
+    with pytest.raises(R.RtgError):
+        ctx.set_semantics(7)
+    ctx.close()

@@ -272,3 +272,57 @@ def test_shadow_masks_cull(hostsim, golden, name):
     f.restype = ctypes.c_long
     bits = f(P(sph), len(sph), P(lg), len(lg))
     assert 0 < bits <= 0.3 * len(sph) * len(sph) * len(lg), bits
+
+
+# ------------------------------------------------------------ OpenCL semantics
+REF_GPU_PPM = "/root/reference/raytracer_gamma/testPPM.ppm"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_GPU_PPM), reason="reference checkout absent")
+def test_opencl_semantics_approach_the_reference_gpu_image(oracle, rtg):
+    """The reference's committed testPPM.ppm was made by its OpenCL kernel on
+    the author's GPU (relaxed division/sqrt, FP contraction), so no IEEE
+    restatement reproduces it bit for bit.  The OpenCL-semantics oracle at the
+    .cl's stack size 5 comes within 3,978 px (max 18 levels) of it, against
+    25,726 px for the CPU path as shipped (S = 6) and 10,102 px for the CPU
+    path at S = 5.  Read in place (never copied into the repo)."""
+    W, H = 800, 600
+    raw = open(REF_GPU_PPM, "rb").read()
+    ref = np.frombuffer(raw[-W * H * 3:], np.uint8).reshape(H, W, 3).astype(int)
+    sph, lg = rtg.reference_scene()
+
+    def diff(fb):
+        b = np.frombuffer(rtg.ppm_file_bytes(fb)[-W * H * 3:], np.uint8).reshape(H, W, 3)
+        d = np.abs(b.astype(int) - ref).max(axis=2)
+        return int((d > 0).sum()), int(d.max())
+
+    assert diff(oracle.render_cl(sph, lg, W, H, 5)) == (3978, 18)
+    assert diff(oracle.render(sph, lg, W, H, 6))[0] == 25726
+    assert diff(oracle.render(sph, lg, W, H, 5))[0] == 10102
+
+
+def test_kernel_traversal_opencl_semantics(hostsim, oracle, rtg, golden):
+    """The kernel's traversal with kCL (variant 50 in the host build) equals
+    the OpenCL-semantics oracle bit for bit."""
+    hostsim.hostsim_set_variant(50)
+    try:
+        rng = np.random.default_rng(505)
+        for trial in range(30):
+            S = int(rng.integers(1, 13))
+            n, m = int(rng.integers(0, 14)), int(rng.integers(0, 5))
+            W, H = int(rng.integers(1, 40)), int(rng.integers(1, 30))
+            aa = float(rng.choice([1.0, 2.0, 3.0, 2.5]))
+            zoom = float(rng.choice([-4.0, -2.0, 3.0]))
+            sph, lg = random_scene(rng, n, m)
+            if zoom > 0:
+                sph["pos"][:, 2] *= -1.0
+            want = oracle.render_cl(sph, lg, W, H, S, aa=aa, zoom=zoom)
+            got = _hostsim_render(hostsim, sph, lg, W, H, S, aa=aa, zoom=zoom)
+            assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
+        sph, lg = rtg.reference_scene()
+        want = oracle.render_cl(sph, lg, 96, 72, 5)
+        assert not bits_equal(want, oracle.render(sph, lg, 96, 72, 5))  # the modes differ
+        got = _hostsim_render(hostsim, sph, lg, 96, 72, 5)
+        assert bits_equal(got, want), first_mismatch(got, want)
+    finally:
+        hostsim.hostsim_set_variant(0)
