@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "rtg.h"
 
 static void check(int rc, const char* what) {
@@ -41,6 +43,8 @@ static void usage() {
   printf("      --scene      FILE    Load the scene from FILE (format: include/rtg.h)\n");
   printf("      --save-scene FILE    Write the scene used to FILE\n");
   printf("      --gpus       N       Render on devices 0..N-1 (row-cyclic shards, RCCL gather)\n");
+  printf("      --semantics  MODE    cpu (default: raytracer.h, bit-exact) or opencl\n");
+  printf("                           (raytrace_kernel.cl; use with --depth 4 = its stack of 5)\n");
   printf("\n");
 }
 
@@ -58,6 +62,7 @@ int main(int argc, char** argv) {
   float aa = 3.f, zoom = -4.f;
   std::string out = "testPPM.ppm", sceneIn, sceneOut;
   unsigned gpus = 0;
+  int semantics = RTG_SEMANTICS_CPU;
   for (int i = 1; i < argc; ++i) {
     auto need = [&](const char* opt) -> const char* {
       if (++i >= argc) {
@@ -108,6 +113,11 @@ int main(int argc, char** argv) {
       sceneIn = need(a);
     } else if (!strcmp(a, "--save-scene")) {
       sceneOut = need(a);
+    } else if (!strcmp(a, "--semantics")) {
+      const char* v = need(a);
+      if (!strcmp(v, "cpu")) semantics = RTG_SEMANTICS_CPU;
+      else if (!strcmp(v, "opencl")) semantics = RTG_SEMANTICS_OPENCL;
+      else { printf("Invalid semantics %s (cpu|opencl)\n", v); return 1; }
     } else if (!strcmp(a, "--gpus")) {
       if (!parse_uint(need(a), &gpus) || gpus == 0) { printf("Invalid GPU count\n"); return 1; }
     } else {
@@ -145,7 +155,24 @@ int main(int argc, char** argv) {
   double best = 1e30;
   for (unsigned r = 0; r < repeat; ++r) {
     auto t0 = std::chrono::steady_clock::now();
-    if (gpus) {
+    if (semantics != RTG_SEMANTICS_CPU) {  // persistent context: semantics is per context
+      if (gpus) { printf("--semantics opencl renders on one device\n"); return 1; }
+      rtg_context* ctx = nullptr;
+      check(rtg_context_create((int)device, &ctx), "rtg_context_create");
+      check(rtg_context_set_semantics(ctx, semantics), "rtg_context_set_semantics");
+      check(rtg_context_set_scene(ctx, spheres.data(), nSph, lights.data(), nLgt),
+            "rtg_context_set_scene");
+      rtg_vec* d = nullptr;
+      if (hipMalloc(&d, pixels.size() * sizeof(rtg_vec)) != hipSuccess)
+        check(RTG_ERR_NOMEM, "hipMalloc");
+      check(rtg_render_device(ctx, W, H, zoom, aa, (int)depth + 1, 16, 0, 1, d, nullptr),
+            "rtg_render_device");
+      if (hipMemcpy(pixels.data(), d, pixels.size() * sizeof(rtg_vec),
+                    hipMemcpyDeviceToHost) != hipSuccess)
+        check(RTG_ERR_HIP, "readback");
+      (void)hipFree(d);
+      rtg_context_destroy(ctx);
+    } else if (gpus) {
       std::vector<int> devs(gpus);
       for (unsigned g = 0; g < gpus; ++g) devs[g] = (int)g;
       float tm[3];

@@ -379,3 +379,19 @@ def test_opencl_semantics_vs_oracle(R, oracle, torch_cuda):
     with pytest.raises(R.RtgError):
         ctx.set_semantics(7)
     ctx.close()
+
+
+def test_host_driver_opencl_semantics_ppm(R, oracle, tmp_path):
+    """rtg_main --semantics opencl --depth 4 (the .cl's stack of 5): its PPM is
+    the OpenCL-semantics oracle's PPM byte for byte."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "raytracer-gamma_amd", "rtg_main")
+    out = str(tmp_path / "cl.ppm")
+    r = subprocess.run([exe, "--semantics", "opencl", "--depth", "4", "--width", "200",
+                        "--height", "150", "--out", out], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    sph, lg = R.reference_scene()
+    want = R.ppm_file_bytes(oracle.render_cl(sph, lg, 200, 150, 5))
+    assert open(out, "rb").read() == want
