@@ -102,6 +102,17 @@ int rtg_render_multi(const int* devices, int nDevices, const rtg_sphere* spheres
                      unsigned sphNum, const rtg_light* lights, unsigned lgtNum,
                      unsigned width, unsigned height, float zoom, float aliasFactor,
                      int stackSize, unsigned rowBlock, rtg_vec* dstHost, float* timingsMs);
+/* The same with a persistent multi-device handle: the RCCL communicator
+ * (ncclCommInitAll, ~0.5 s), the per-device contexts, streams and buffers
+ * are kept across frames.  Not re-entrant per handle. */
+typedef struct rtg_multi rtg_multi;
+int rtg_multi_create(const int* devices, int nDevices, rtg_multi** out);
+int rtg_multi_set_scene(rtg_multi* mg, const rtg_sphere* spheres, unsigned sphNum,
+                        const rtg_light* lights, unsigned lgtNum);
+int rtg_multi_render(rtg_multi* mg, unsigned width, unsigned height, float zoom,
+                     float aliasFactor, int stackSize, unsigned rowBlock, rtg_vec* dstHost,
+                     float* timingsMs);
+int rtg_multi_destroy(rtg_multi* mg);
 
 /* ---- persistent context: scene resident in HBM, caller-owned streams ---- */
 typedef struct rtg_context rtg_context;

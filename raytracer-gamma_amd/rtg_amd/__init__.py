@@ -57,6 +57,7 @@ EXPORTED = [
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate", "rtg_assemble_shards_device",
     "rtg_render_multi", "rtg_scene_load", "rtg_scene_save", "rtg_context_set_semantics",
+    "rtg_multi_create", "rtg_multi_set_scene", "rtg_multi_render", "rtg_multi_destroy",
 ]
 
 
@@ -101,6 +102,10 @@ def lib() -> ctypes.CDLL:
         L.rtg_ppm_bytes_device.argtypes = [vp, vp, sz, vp, vp, vp]
         L.rtg_assemble_shards_device.argtypes = [vp, vp, u, u, u, u, u, vp, vp]
         L.rtg_render_multi.argtypes = [vp, i, vp, u, vp, u, u, u, f, f, i, u, vp, vp]
+        L.rtg_multi_create.argtypes = [vp, i, ctypes.POINTER(vp)]
+        L.rtg_multi_set_scene.argtypes = [vp, vp, u, vp, u]
+        L.rtg_multi_render.argtypes = [vp, u, u, f, f, i, u, vp, vp]
+        L.rtg_multi_destroy.argtypes = [vp]
         pu = ctypes.POINTER(u)
         L.rtg_scene_load.argtypes = [ctypes.c_char_p, vp, u, pu, vp, u, pu]
         L.rtg_scene_save.argtypes = [ctypes.c_char_p, vp, u, vp, u]
@@ -248,6 +253,42 @@ def render_multi(spheres, lights, width: int, height: int, devices=(0,), zoom: f
                                   float(alias_factor), stack_size, row_block, _ptr(out),
                                   _ptr(tm)), "rtg_render_multi")
     return out, [float(v) for v in tm]
+
+
+class MultiContext:
+    """Persistent multi-device handle (rtg_multi_*): RCCL communicator, contexts,
+    streams and buffers kept across frames."""
+
+    def __init__(self, devices=(0,)):
+        self._h = ctypes.c_void_p()
+        self._devs = np.ascontiguousarray(devices, np.int32)
+        _check(lib().rtg_multi_create(_ptr(self._devs), len(self._devs), ctypes.byref(self._h)),
+               "rtg_multi_create")
+
+    def set_scene(self, spheres, lights):
+        self._sph = np.ascontiguousarray(spheres, SPHERE_DTYPE)
+        self._lgt = np.ascontiguousarray(lights, LIGHT_DTYPE)
+        _check(lib().rtg_multi_set_scene(self._h, _ptr(self._sph), len(self._sph),
+                                         _ptr(self._lgt), len(self._lgt)), "rtg_multi_set_scene")
+
+    def render(self, width, height, zoom=-4.0, alias_factor=3.0, stack_size=6, row_block=16):
+        out = np.empty((height, width, 3), np.float32)
+        tm = np.zeros(3, np.float32)
+        _check(lib().rtg_multi_render(self._h, width, height, float(zoom), float(alias_factor),
+                                      stack_size, row_block, _ptr(out), _ptr(tm)),
+               "rtg_multi_render")
+        return out, [float(v) for v in tm]
+
+    def close(self):
+        if self._h:
+            lib().rtg_multi_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def render_rows(spheres, lights, width: int, height: int, rows, zoom: float = -4.0,

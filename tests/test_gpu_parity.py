@@ -317,6 +317,15 @@ def test_render_multi_one_process(R, golden):
                                 row_block=B)
         assert canon_md5(fb) == c["fb_md5"], (devs, B)
         assert tm[0] > 0 and tm[2] >= tm[0]
+    # persistent handle: several frames and sizes, one communicator
+    mc = R.MultiContext(devs)
+    mc.set_scene(sph, lg)
+    for _ in range(2):
+        fb, tm = mc.render(c["W"], c["H"], stack_size=c["stack_size"])
+        assert canon_md5(fb) == c["fb_md5"]
+    small, _ = mc.render(40, 30, stack_size=c["stack_size"])
+    assert bits_equal(small, R.render(sph, lg, 40, 30, stack_size=c["stack_size"]))
+    mc.close()
     with pytest.raises(R.RtgError):
         R.render_multi(sph, lg, 8, 8, devices=[0, 0])
     with pytest.raises(R.RtgError):
