@@ -34,7 +34,8 @@ except Exception:  # torch absent: librtg loads /opt/rocm's runtime itself
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "librtg.so")
+# RTG_LIB: an alternative build of the same library (compiler-flag A/B runs).
+LIB_PATH = os.environ.get("RTG_LIB") or os.path.join(os.path.dirname(_HERE), "librtg.so")
 
 VEC_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4")])
 MATERIAL_DTYPE = np.dtype([("matteColour", "<f4", 3), ("glossColour", "<f4", 3),
