@@ -44,4 +44,22 @@ RTG_HDI unsigned char ppm_byte(float c, float mx) {
   return (unsigned char)(i & 0xFF);
 }
 
+#if defined(__HIPCC__)
+// Restores the caller's current HIP device when an ABI entry point returns:
+// the entry points call hipSetDevice for their context's device, and a torch
+// (or any HIP) caller must not find its later allocations and launches moved
+// to another GPU.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#endif
+
 }  // namespace rtg

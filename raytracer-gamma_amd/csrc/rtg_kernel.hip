@@ -183,6 +183,7 @@ int rtg_device_info(int device, char* buf, size_t buflen) {
 }
 
 int rtg_context_create(int device, rtg_context** out) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!out) return RTG_ERR_INVALID;
   *out = nullptr;
@@ -195,7 +196,17 @@ int rtg_context_create(int device, rtg_context** out) {
   HIP_TRY(hipSetDevice(device));
   rtg_context* c = new rtg_context();
   c->device = device;
-  if (const char* v = getenv("RTG_VARIANT")) c->opts.variant = atoi(v);  // A/B knob
+  if (const char* v = getenv("RTG_VARIANT")) {  // A/B knob
+    char* end = nullptr;
+    const long var = strtol(v, &end, 10);
+    const VariantInfo* vi = (end != v && *end == '\0') ? variant_info((int)var) : nullptr;
+    if (!vi || vi->semantic) {
+      delete c;
+      rtg_set_error("RTG_VARIANT=%s is not a launch variant", v);
+      return RTG_ERR_INVALID;
+    }
+    c->opts.variant = (int)var;
+  }
   if (hipMalloc(&c->maxScratch, 4) != hipSuccess) {
     delete c;
     rtg_set_error("hipMalloc failed");
@@ -206,6 +217,7 @@ int rtg_context_create(int device, rtg_context** out) {
 }
 
 int rtg_context_destroy(rtg_context* ctx) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx) return RTG_OK;
   (void)hipSetDevice(ctx->device);
@@ -218,6 +230,7 @@ int rtg_context_destroy(rtg_context* ctx) {
 }
 
 int rtg_diag_read(rtg_context* ctx, unsigned long long* out, int reset) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || !out) return RTG_ERR_INVALID;
   if (!ctx->diag) {
@@ -232,6 +245,7 @@ int rtg_diag_read(rtg_context* ctx, unsigned long long* out, int reset) {
 }
 
 int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* count) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || (cap && !out4) || !count) return RTG_ERR_INVALID;
   *count = ctx->timelineCount;
@@ -256,12 +270,22 @@ int rtg_context_set_semantics(rtg_context* ctx, int semantics) {
 int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts) {
   rtg_clear_error();
   if (!ctx || !opts) return RTG_ERR_INVALID;
+  const VariantInfo* vi = variant_info(opts->variant);
+  if (!vi || vi->semantic) {  // semantic variants: rtg_context_set_semantics only
+    rtg_set_error("rtg_set_launch_opts: unknown kernel variant %d", opts->variant);
+    return RTG_ERR_INVALID;
+  }
+  if (opts->flags & ~RTG_LAUNCH_TIMELINE) {
+    rtg_set_error("rtg_set_launch_opts: unknown flags 0x%x", (unsigned)opts->flags);
+    return RTG_ERR_INVALID;
+  }
   ctx->opts = *opts;
   return RTG_OK;
 }
 
 int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned sphNum,
                           const rtg_light* lights, unsigned lgtNum) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || (sphNum && !spheres) || (lgtNum && !lights)) {
     rtg_set_error("rtg_context_set_scene: invalid arguments");
@@ -319,13 +343,20 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   KernelArgs a;
   int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
   if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));  // before any allocation below
   int variant = ctx->opts.variant;
-  // sample-parallel kernels need all of a pixel's samples in one wave
   if (ctx->semantics == RTG_SEMANTICS_OPENCL) variant = 50;  // results differ: not a knob
-  auto isSample = [](int v) { return v == 0 || (v >= 14 && v <= 19) || v == 50 || v == 110; };
-  if (isSample(variant) && (a.cam.nAA < 1 || a.cam.nAA > 8))
+  const VariantInfo* vi = variant_info(variant);
+  if (!vi) {
+    rtg_set_error("render: unknown kernel variant %d", variant);
+    return RTG_ERR_INVALID;
+  }
+  // sample-parallel kernels need all of a pixel's samples in one wave
+  if (vi->kind == kVariantSample && (a.cam.nAA < 1 || a.cam.nAA > 8)) {
     variant = variant == 110 ? 100 : variant == 50 ? 59 : 9;
-  const bool sampleKernel = isSample(variant);
+    vi = variant_info(variant);
+  }
+  const bool sampleKernel = vi->kind == kVariantSample;
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
   if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 50 ||
@@ -333,7 +364,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant);
   if (!fn) {
-    rtg_set_error("stackSize %d outside [1, %d]", stackSize, RTG_MAX_STACK);
+    rtg_set_error("no kernel for stackSize %d (valid: 1..%d), variant %d", stackSize,
+                  RTG_MAX_STACK, variant);
     return RTG_ERR_INVALID;
   }
   unsigned rows;
@@ -375,7 +407,6 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     }
     a.diag = ctx->diag;
   }
-  HIP_TRY(hipSetDevice(ctx->device));
   unsigned threads = (unsigned)kBlock;
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
   if (sampleKernel) {
@@ -414,6 +445,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
 int rtg_render_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
                       float aliasFactor, int stackSize, unsigned rowBlock, unsigned shard,
                       unsigned nShards, rtg_vec* dstDevice, void* stream) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   return launch_trace(ctx, width, height, zoom, aliasFactor, stackSize, rowBlock, shard,
                       nShards, nullptr, 0, dstDevice, stream);
@@ -422,6 +454,7 @@ int rtg_render_device(rtg_context* ctx, unsigned width, unsigned height, float z
 int rtg_render_rows_device(rtg_context* ctx, unsigned width, unsigned height, float zoom,
                            float aliasFactor, int stackSize, const unsigned* rowsDevice,
                            unsigned nRows, rtg_vec* dstDevice, void* stream) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (nRows && !rowsDevice) {
     rtg_set_error("rtg_render_rows_device: null row list");
@@ -436,6 +469,7 @@ int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
                     const rtg_light* lights, unsigned lgtNum, unsigned width, unsigned height,
                     float zoom, float aliasFactor, int stackSize, const unsigned* rows,
                     unsigned nRows, rtg_vec* dstHost) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (nRows && (!rows || !dstHost)) {
     rtg_set_error("rtg_render_rows: null argument");
@@ -487,6 +521,7 @@ int rtg_render_rows(int device, const rtg_sphere* spheres, unsigned sphNum,
 
 int rtg_max_colour_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n,
                           float* maxDevice, void* stream) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || !maxDevice || (n && !pixelsDevice)) return RTG_ERR_INVALID;
   HIP_TRY(hipSetDevice(ctx->device));
@@ -508,6 +543,7 @@ int rtg_max_colour_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t 
 int rtg_assemble_shards_device(rtg_context* ctx, const rtg_vec* gathered, unsigned nShards,
                                unsigned paddedRows, unsigned width, unsigned height,
                                unsigned rowBlock, rtg_vec* frame, void* stream) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || !gathered || !frame || nShards == 0 || rowBlock == 0 || width == 0 ||
       height == 0) {
@@ -548,6 +584,7 @@ int rtg_assemble_shards_device(rtg_context* ctx, const rtg_vec* gathered, unsign
 
 int rtg_ppm_bytes_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n,
                          const float* maxDevice, unsigned char* outDevice, void* stream) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || !maxDevice || (n && (!pixelsDevice || !outDevice))) return RTG_ERR_INVALID;
   if (n == 0) return RTG_OK;
@@ -564,6 +601,7 @@ int rtg_ppm_bytes_device(rtg_context* ctx, const rtg_vec* pixelsDevice, size_t n
 int rtg_render(int device, const rtg_sphere* spheres, unsigned sphNum, const rtg_light* lights,
                unsigned lgtNum, unsigned width, unsigned height, float zoom, float aliasFactor,
                int stackSize, rtg_vec* dstHost) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   int rc0 = check_render_args(spheres, sphNum, lights, lgtNum, width, height, zoom, aliasFactor,
                               stackSize, dstHost);

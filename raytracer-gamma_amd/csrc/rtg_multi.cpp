@@ -49,6 +49,7 @@ struct rtg_multi {
 extern "C" {
 
 int rtg_multi_destroy(rtg_multi* mg) {
+  rtg::DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!mg) return RTG_OK;
   for (Dev& v : mg->d)
@@ -73,6 +74,7 @@ int rtg_multi_destroy(rtg_multi* mg) {
 }
 
 int rtg_multi_create(const int* devices, int nDevices, rtg_multi** out) {
+  rtg::DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!out || !devices || nDevices < 1) {
     rtg_set_error("rtg_multi_create: invalid arguments");
@@ -132,6 +134,7 @@ int rtg_multi_create(const int* devices, int nDevices, rtg_multi** out) {
 
 int rtg_multi_set_scene(rtg_multi* mg, const rtg_sphere* spheres, unsigned sphNum,
                         const rtg_light* lights, unsigned lgtNum) {
+  rtg::DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!mg) {
     rtg_set_error("rtg_multi_set_scene: null handle");
@@ -149,6 +152,7 @@ int rtg_multi_set_scene(rtg_multi* mg, const rtg_sphere* spheres, unsigned sphNu
 int rtg_multi_render(rtg_multi* mg, unsigned width, unsigned height, float zoom,
                      float aliasFactor, int stackSize, unsigned rowBlock, rtg_vec* dstHost,
                      float* timingsMs) {
+  rtg::DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!mg || !mg->hasScene || !dstHost || rowBlock == 0 || width == 0 || height == 0) {
     rtg_set_error("rtg_multi_render: invalid arguments (or no scene)");

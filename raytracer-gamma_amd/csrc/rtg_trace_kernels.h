@@ -497,6 +497,31 @@ void trace_samples_kernel(const KernelArgs a) {
 //   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9,
 //     110 = the default sample kernel (0)
+// The one table of valid variants and their kernel kind; anything else is
+// rejected (rtg_set_launch_opts, RTG_VARIANT) and trace_fn returns nullptr.
+// kSemantic variants change results and are only chosen through
+// rtg_context_set_semantics, never accepted as a launch option.
+enum VariantKind : int { kVariantInvalid = 0, kVariantTile = 1, kVariantSample = 2 };
+struct VariantInfo {
+  int variant;
+  int kind;
+  bool semantic;
+};
+constexpr VariantInfo kVariants[] = {
+    {0, kVariantSample, false},  {1, kVariantTile, false},    {2, kVariantTile, false},
+    {3, kVariantTile, false},    {4, kVariantTile, false},    {5, kVariantTile, false},
+    {6, kVariantTile, false},    {8, kVariantTile, false},    {9, kVariantTile, false},
+    {14, kVariantSample, false}, {15, kVariantSample, false}, {16, kVariantSample, false},
+    {17, kVariantSample, false}, {18, kVariantSample, false}, {19, kVariantSample, false},
+    {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
+    {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
+};
+inline const VariantInfo* variant_info(int v) {
+  for (const VariantInfo& i : kVariants)
+    if (i.variant == v) return &i;
+  return nullptr;
+}
+
 template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
@@ -529,7 +554,8 @@ static TraceFn trace_fn(bool lds, int variant) {
     case 108: return trace_fn_v<S, 108>(lds);
     case 2: return trace_fn_v<S, 2>(lds);
     case 3: return trace_fn_v<S, 3>(lds);
-    default: return trace_fn_v<S, 0>(lds);
+    case 0: return trace_fn_v<S, 0>(lds);
+    default: return nullptr;  // not in kVariants
   }
 }
 

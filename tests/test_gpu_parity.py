@@ -305,13 +305,10 @@ def test_wave_timeline_diagnostic(R, golden, torch_cuda, variant):
     ctx.close()
 
 
-def test_render_multi_one_process(R, golden):
-    """rtg_render_multi (one process, RCCL gather over the listed devices) on
-    the devices visible here: bit-identical to the golden frame."""
+def _render_multi_checks(R, golden, devs):
     c = golden["configs"]["c2"]
     sph, lg = load_scene("c2", c["spheres"], c["lights"])
     n = R.device_count()
-    devs = list(range(min(n, 8)))
     for B in (16, 8):
         fb, tm = R.render_multi(sph, lg, c["W"], c["H"], devices=devs, stack_size=c["stack_size"],
                                 row_block=B)
@@ -330,6 +327,78 @@ def test_render_multi_one_process(R, golden):
         R.render_multi(sph, lg, 8, 8, devices=[0, 0])
     with pytest.raises(R.RtgError):
         R.render_multi(sph, lg, 8, 8, devices=[n + 3])
+
+
+def test_render_multi_one_device(R, golden):
+    """rtg_render_multi (one process, RCCL gather) with one device: the
+    communicator has size 1, so this covers the render/gather/assemble code
+    path but not a multi-rank gather."""
+    _render_multi_checks(R, golden, [0])
+
+
+def test_render_multi_several_devices(R, golden):
+    """The same over every visible device (up to 8): the real multi-rank
+    ncclGather.  Skipped, visibly, on a box with fewer than two GPUs."""
+    n = R.device_count()
+    if n < 2:
+        pytest.skip(f"multi-device RCCL gather needs >= 2 GPUs ({n} visible): unverified here")
+    _render_multi_checks(R, golden, list(range(min(n, 8))))
+
+
+def test_unknown_variant_is_rejected(R, torch_cuda):
+    """rtg_set_launch_opts accepts only the variants of the kernel table; the
+    OpenCL-semantics variants (50, 59) change results and are reachable only
+    through rtg_context_set_semantics."""
+    ctx = R.Context(0)
+    for bad in (7, 10, 13, 20, 21, 50, 59, 101, 105, 109, -1, 1 << 20):
+        with pytest.raises(R.RtgError):
+            ctx.set_variant(bad)
+    with pytest.raises(R.RtgError):
+        ctx.set_variant(0, 0x100)  # unknown flag bit
+    # the context still renders with its previous (default) variant
+    sph, lg = R.reference_scene()
+    ctx.set_scene(sph, lg)
+    out = torch_cuda.empty((12, 16, 3), dtype=torch_cuda.float32, device="cuda")
+    ctx.render_device(16, 12, out.data_ptr())
+    torch_cuda.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), R.render(sph, lg, 16, 12))
+    ctx.close()
+    old = os.environ.get("RTG_VARIANT")
+    try:
+        for bad in ("7", "50", "x", ""):
+            os.environ["RTG_VARIANT"] = bad
+            with pytest.raises(R.RtgError):
+                R.Context(0)
+        os.environ["RTG_VARIANT"] = "9"
+        R.Context(0).close()
+    finally:
+        if old is None:
+            os.environ.pop("RTG_VARIANT", None)
+        else:
+            os.environ["RTG_VARIANT"] = old
+
+
+def test_current_device_is_restored(R, golden, torch_cuda):
+    """ABI calls select their context's device and restore the caller's
+    current device on return (checked on the last visible device when there
+    are several)."""
+    torch = torch_cuda
+    n = R.device_count()
+    cur = n - 1
+    torch.cuda.set_device(cur)
+    try:
+        sph, lg = R.reference_scene()
+        R.render(sph, lg, 8, 6, device=0)
+        assert torch.cuda.current_device() == cur
+        R.render_multi(sph, lg, 8, 6, devices=list(range(min(n, 8))))
+        assert torch.cuda.current_device() == cur
+        ctx = R.Context(0)
+        ctx.set_scene(sph, lg)
+        assert torch.cuda.current_device() == cur
+        ctx.close()
+        assert torch.cuda.current_device() == cur
+    finally:
+        torch.cuda.set_device(0)
 
 
 @pytest.mark.parametrize("extra", [[], ["--gpus", "1"]])
