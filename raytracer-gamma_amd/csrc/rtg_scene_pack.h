@@ -83,6 +83,17 @@ inline float guard_r2(const rtg_sphere& s) {
   return f;
 }
 
+// Radius of the ball around c_h that holds every refraction test point
+// P + 0.01f D (raytracer.h:690) with P in the guard ball B_h and
+// |D| <= kContainDirMax (1 + 2^-20): 0.01 |D| with the float product's and
+// the comparison's rounding, plus the rounding of the sum, below
+// 2^-16 (|c_h| + g_h + 1).
+inline double contain_reach(const rtg_sphere& s) {
+  const double g = guard_radius(s);
+  const double c = fabs((double)s.pos.x) + fabs((double)s.pos.y) + fabs((double)s.pos.z);
+  return g + 0.01 * (double)kContainDirMax * (1.0 + 0x1p-16) + 0x1p-16 * (c + g + 1.0);
+}
+
 inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                          unsigned m, std::vector<unsigned>* out) {
   out->clear();
@@ -134,25 +145,35 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
       }
     }
   }
-  // Overlap masks (closest_enter, rtg_trace.h): bit j of mask h is set when
-  // ball j grown by mu_j = 2^-8 (|c_j - c_h| + g_h + r_j) meets the guard ball
-  // B_h.  A ray whose origin and computed exit point from sphere h both lie in
-  // B_h stays inside B_h up to that exit, so a sphere outside the mask has no
-  // accepted root before it (same error argument as above): the closest hit
-  // is h or an overlap sphere.
+  // Overlap masks (closest_enter and primary_container_sel, rtg_trace.h): bit
+  // j of mask h is set when ball(c_j, |r_j| + 1e-6) grown by
+  // mu_j = 2^-8 (|c_j - c_h| + g_h + r_j) meets the ball B'_h = ball(c_h,
+  // contain_reach(h)) around the guard ball B_h (and always for j == h).
+  //  * closest_enter: a ray whose origin and computed exit point from sphere h
+  //    both lie in B_h stays inside B_h up to that exit, so a sphere outside
+  //    the mask has no accepted root before it (same error argument as
+  //    above): the closest hit is h or a mask sphere.
+  //  * primary_container_sel: the refraction test point P + 0.01f D
+  //    (raytracer.h:690) of a hit point P in B_h with |D| <= kContainDirMax
+  //    lies in B'_h (the reach covers 0.01 |D| and the rounding of the point),
+  //    and the float containment test (raytracer.h:255-264) cannot accept a
+  //    point more than mu_j outside ball(c_j, |r_j| + 1e-6); so the first
+  //    containing sphere in index order is the first containing mask sphere.
   for (unsigned h = 0; h < n; ++h) {
     const rtg_sphere& sh = spheres[h];
     const double g = guard_radius(sh);
+    const double reach = contain_reach(sh);
     unsigned* w = &(*out)[((size_t)m * n + h) * 2];
+    w[h >> 5] |= 1u << (h & 31);
     for (unsigned j = 0; j < n; ++j) {
       if (j == h) continue;
       const rtg_sphere& sj = spheres[j];
       const double dx = (double)sj.pos.x - sh.pos.x, dy = (double)sj.pos.y - sh.pos.y,
                    dz = (double)sj.pos.z - sh.pos.z;
       const double d = sqrt(dx * dx + dy * dy + dz * dz);
-      const double rj = fabs((double)sj.radius);
+      const double rj = fabs((double)sj.radius) + 1e-6;
       const double mu = 0x1p-8 * (d + g + rj);
-      if (!(d > (g + rj + mu) * (1.0 + 1e-9))) w[j >> 5] |= 1u << (j & 31);
+      if (!(d > (reach + rj + mu) * (1.0 + 1e-9))) w[j >> 5] |= 1u << (j & 31);
     }
   }
 }

@@ -233,6 +233,31 @@ RTG_HD int primary_container(const Scene& sc, V3 pt) {
   return found;
 }
 
+// Direction length bound of the masked containment test: a lane uses its hit
+// sphere's overlap mask for primary_container only when |D|^2 <= this^2
+// (computed in float; primary, reflection and refraction directions are
+// about unit length).  See contain_reach (rtg_scene_pack.h).
+constexpr float kContainDirMax = 3.0f;
+
+// primary_container over a wave-uniform subset `sel` of spheres 0..63 (the
+// union of the active lanes' overlap masks, shadow_masks in rtg_scene_pack.h):
+// every sphere outside `sel` provably fails the containment test for this
+// point, so the first containing sphere of `sel` in index order is the
+// reference's answer.  One scalar load of a containment record per sphere.
+template <class Scene>
+RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel) {
+  int found = -1;
+  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+    const unsigned i = (unsigned)__builtin_ctzll(m);
+    float cr;
+    const V3 c = sc.sphere_contain(i, cr);
+    const V3 dist = vsub(pt, c);
+    if (found < 0 && vdot(dist, dist) <= cr) found = (int)i;
+    if (sc.all(found >= 0)) break;
+  }
+  return found;
+}
+
 // Query strategies (defined below): see query_closest / query_blocked.
 template <int Q, class Scene>
 RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t);
@@ -303,9 +328,12 @@ RTG_HD float polarised_reflection(float n1, float n2, float cosA1, float cosA2) 
 
 // raytracer.h:642-815.  Computes the reflection factor R and, when wantRay,
 // the refracted direction.  Returns the target material index.
+// hit >= 0: the sphere P lies on, and guardOK: P passed its guard-ball test;
+// then (scenes with masks) the refraction target's containment test runs over
+// the wave's union of overlap masks (primary_container_sel).
 template <bool kCL = false, class Scene>
 RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRay,
-                      V3& dirOut, float& R) {
+                      V3& dirOut, float& R, int hit = -1, bool guardOK = false) {
   float cosA1 = vdot(D, N);
   float sinA1 = 0.f;
   if (cosA1 <= -1.0f) { cosA1 = -1.f; sinA1 = 0.f; }
@@ -314,7 +342,13 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }
 
   const V3 testPt = vadd(vsmul(0.01f, D), P);
-  int tgt = primary_container(sc, testPt);
+  int tgt;
+  if (hit >= 0 && sc.has_smask()) {
+    const bool ok = guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax;
+    tgt = primary_container_sel(sc, testPt, sc.contain_union(hit, ok));
+  } else {
+    tgt = primary_container(sc, testPt);
+  }
   if (tgt < 0) tgt = (int)sc.n;  // background material
   const float nTgt = sc.refr(tgt);
   const float ratio = nSrc / nTgt;
@@ -406,15 +440,15 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       const float op = mh.opacity;
       const float tr = 1.f - op;
       V3 colour = v3(0.f, 0.f, 0.f);
+      bool guardOK = false;
+      if constexpr (Q == 4) {  // P in the hit sphere's guard ball (shadow/overlap masks)
+        const V3 e = vsub(P, c);
+        guardOK = vdot(e, e) <= sc.guard_r2((unsigned)hit);
+      }
       if (op > 0.f) {
         V3 tmp = vmul(I, mh.matte);
         tmp = vsmul(op, tmp);
         sc.probe_begin(kProbeMatte);
-        bool guardOK = false;
-        if constexpr (Q == 4) {  // P in the hit sphere's guard ball (shadow masks)
-          const V3 e = vsub(P, c);
-          guardOK = vdot(e, e) <= sc.guard_r2((unsigned)hit);
-        }
         const V3 mc = matte_light<Q>(sc, P, N, hit, guardOK);
         sc.probe_end(kProbeMatte);
         tmp = vmul(mc, tmp);
@@ -426,7 +460,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         V3 cdir;
         float R;
         sc.probe_begin(kProbeRefraction);
-        const int tgt = refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R);
+        const int tgt = Q == 4 ? refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R, hit, guardOK)
+                               : refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R);
         sc.probe_end(kProbeRefraction);
         // stage-1 reflection colour, raytracer.h:563-578
         const float prod = tr * R;
@@ -737,7 +772,7 @@ RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, boo
   ok = res && th < 1000.f && vdot(e0, e0) <= g2 && vdot(e1, e1) <= g2;
   float minT = 1000.f;
   int best = -1;
-  uint64_t ov = ok ? sc.overlap_mask((unsigned)h) : 0ull;
+  uint64_t ov = ok ? (sc.overlap_mask((unsigned)h) & ~(1ull << h)) : 0ull;
   bool hDone = false;
   for (;;) {  // candidates in index order; h's result is already known
     const unsigned j = ov ? (unsigned)__builtin_ctzll(ov) : 64u;

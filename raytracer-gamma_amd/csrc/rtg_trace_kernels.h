@@ -105,6 +105,9 @@ struct DevScene {
   __device__ __forceinline__ V3 sphere_screen(unsigned i, float& rs) const {
     return sphere(n4 + 4 + i, rs);
   }
+  __device__ __forceinline__ V3 sphere_contain(unsigned i, float& cr) const {
+    return sphere(2 * (n4 + 4) + i, cr);
+  }
   // Shadow and overlap masks (rtg_scene_pack.h shadow_masks): n <= 64.
   __device__ __forceinline__ bool has_smask() const { return smask != nullptr; }
   __device__ __forceinline__ uint64_t overlap_mask(unsigned h) const {  // per lane
@@ -112,21 +115,28 @@ struct DevScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   __device__ __forceinline__ float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
-  // Union of the active lanes' masks for light l (wave-uniform): one pass per
-  // distinct hit sphere among the lanes; every sphere if a lane's hit point
-  // failed its guard test.
-  __device__ __forceinline__ uint64_t shadow_union(unsigned l, int hit, bool guardOK) const {
-    if (__ballot(!guardOK)) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+  // Union of the active lanes' masks of table row `row` (wave-uniform): one
+  // scalar mask load per distinct hit sphere among the lanes; every sphere if
+  // a lane is not `ok` (its hit point failed the guard test).  Row l < m holds
+  // light l's shadow masks, row m the overlap masks.
+  __device__ __forceinline__ uint64_t mask_union(unsigned row, int hit, bool ok) const {
+    if (__ballot(!ok)) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
     uint64_t todo = __ballot(1);
     uint64_t u = 0;
     while (todo) {
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(hit, src);
-      const cuint_p w = smask + 2u * (l * n + (unsigned)h0);
+      const cuint_p w = smask + 2u * (row * n + (unsigned)h0);
       u |= (uint64_t)w[0] | ((uint64_t)w[1] << 32);
       todo &= ~__ballot(hit == h0);
     }
     return u;
+  }
+  __device__ __forceinline__ uint64_t shadow_union(unsigned l, int hit, bool guardOK) const {
+    return mask_union(l, hit, guardOK);
+  }
+  __device__ __forceinline__ uint64_t contain_union(int hit, bool ok) const {
+    return mask_union(m, hit, ok);
   }
   // Per-lane sphere record (divergent index): from the LDS copy.
   __device__ __forceinline__ V3 sphere_lane(unsigned i, float& r2) const {

@@ -45,6 +45,11 @@ struct HostScene {
   void sphere4_screen(unsigned i, rtg::V3* c, float* rs) const { sphere4(n4 + 4 + i, c, rs); }
   rtg::V3 sphere_screen(unsigned i, float& rs) const { return sphere(n4 + 4 + i, rs); }
   void sphere4_contain(unsigned i, rtg::V3* c, float* cr) const { sphere4(2 * (n4 + 4) + i, c, cr); }
+  rtg::V3 sphere_contain(unsigned i, float& cr) const { return sphere(2 * (n4 + 4) + i, cr); }
+  uint64_t contain_union(int hit, bool ok) const {
+    if (!ok) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+    return overlap_mask((unsigned)hit);
+  }
   // shadow masks: a single lane, so the union is that lane's mask
   const unsigned* smask = nullptr;
   bool has_smask() const { return smask != nullptr; }
@@ -377,4 +382,90 @@ extern "C" long hostsim_shadow_mask_bits(const rtg_sphere* spheres, unsigned n,
   long bits = 0;
   for (unsigned w : masks) bits += __builtin_popcount(w);
   return bits;
+}
+
+// Overlap masks as containment candidates (primary_container_sel): for a hit
+// point P in sphere h's guard ball and a direction D with |D|^2 <= 9 (float),
+// the refraction test point P + 0.01f D (raytracer.h:690) is never inside a
+// sphere j outside mask h by the reference's own float test
+// (raytracer.h:255-264).  Random scenes, half of the spheres placed just
+// outside h's containment reach; returns the violations, *tested = points x
+// spheres checked.
+extern "C" long hostsim_contain_mask_check(long scenes, unsigned n, long points,
+                                           unsigned long long seed, long* tested) {
+  unsigned long long st = seed * 0x9E3779B97F4A7C15ull + 11;
+  auto u01 = [&]() {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  };
+  long bad = 0, cnt = 0;
+  std::vector<rtg_sphere> sph(n);
+  for (long sc = 0; sc < scenes; ++sc) {
+    const double scale = pow(10.0, -1.5 + 3.0 * u01());
+    for (unsigned i = 0; i < n; ++i) {
+      memset(&sph[i], 0, sizeof(rtg_sphere));
+      sph[i].pos.x = (float)((u01() - 0.5) * 24 * scale);
+      sph[i].pos.y = (float)((u01() - 0.5) * 16 * scale);
+      sph[i].pos.z = (float)((-6 - 34 * u01()) * scale);
+      sph[i].radius = (float)((0.3 + 3 * u01()) * scale) * (u01() < 0.1 ? -1.f : 1.f);
+    }
+    // half of the spheres: just outside sphere 0's containment reach
+    for (unsigned i = n / 2; i < n; ++i) {
+      const rtg_sphere& h = sph[0];
+      double v[3] = {u01() - 0.5, u01() - 0.5, u01() - 0.5};
+      const double vl = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      const double ri = fabs((double)sph[i].radius) + 1e-6;
+      const double dist = (rtg::contain_reach(h) + ri) * (1.0 + pow(10.0, -5.0 + 3.0 * u01()));
+      sph[i].pos.x = (float)(h.pos.x + dist * v[0] / vl);
+      sph[i].pos.y = (float)(h.pos.y + dist * v[1] / vl);
+      sph[i].pos.z = (float)(h.pos.z + dist * v[2] / vl);
+    }
+    std::vector<unsigned> masks;
+    rtg::shadow_masks(sph.data(), n, nullptr, 0, &masks);
+    if (masks.empty()) continue;  // m = 0: the n overlap masks only
+    for (unsigned h = 0; h < n; ++h) {
+      const unsigned* w = &masks[(size_t)h * 2];
+      const rtg_sphere& sh = sph[h];
+      const double g = rtg::guard_radius(sh);
+      const float G2 = rtg::guard_r2(sh);
+      for (unsigned j = 0; j < n; ++j) {
+        if (w[j >> 5] & (1u << (j & 31))) continue;
+        const float rc = sph[j].radius + 1.0e-6f;
+        const float cr = rc * rc;
+        const rtg::V3 cj = rtg::v3(sph[j].pos.x, sph[j].pos.y, sph[j].pos.z);
+        for (long k = 0; k < points; ++k) {
+          // P in the guard ball, mostly on h's surface facing sphere j; D
+          // pointing at j, up to the length bound
+          double ux = u01() - 0.5, uy = u01() - 0.5, uz = u01() - 0.5;
+          const double cx = (double)cj.x - sh.pos.x, cy = (double)cj.y - sh.pos.y,
+                       cz = (double)cj.z - sh.pos.z;
+          const double cl = sqrt(cx * cx + cy * cy + cz * cz) + 1e-300;
+          if (k & 1) {
+            const double spread = pow(10.0, -3.0 * u01());
+            ux = cx / cl + spread * ux; uy = cy / cl + spread * uy; uz = cz / cl + spread * uz;
+          }
+          const double ul = sqrt(ux * ux + uy * uy + uz * uz);
+          const double rad = (k % 6 == 0) ? g * u01() : g * (1.0 - 1e-3 * u01());
+          const rtg::V3 P = rtg::v3((float)(sh.pos.x + rad * ux / ul),
+                                    (float)(sh.pos.y + rad * uy / ul),
+                                    (float)(sh.pos.z + rad * uz / ul));
+          const rtg::V3 e = rtg::vsub(P, rtg::v3(sh.pos.x, sh.pos.y, sh.pos.z));
+          if (!(rtg::vdot(e, e) <= G2)) continue;  // the kernel scans every sphere then
+          const double dl = rtg::kContainDirMax * (k % 3 == 0 ? u01() : 1.0 - 1e-6 * u01());
+          const double sp = 0.05 * u01();
+          double dx = cx / cl + sp * (u01() - 0.5), dy = cy / cl + sp * (u01() - 0.5),
+                 dz = cz / cl + sp * (u01() - 0.5);
+          const double dn = sqrt(dx * dx + dy * dy + dz * dz);
+          const rtg::V3 D = rtg::v3((float)(dx / dn * dl), (float)(dy / dn * dl), (float)(dz / dn * dl));
+          if (!(rtg::vdot(D, D) <= rtg::kContainDirMax * rtg::kContainDirMax)) continue;
+          const rtg::V3 pt = rtg::vadd(rtg::vsmul(0.01f, D), P);
+          ++cnt;
+          const rtg::V3 dist = rtg::vsub(pt, cj);
+          if (rtg::vdot(dist, dist) <= cr) ++bad;
+        }
+      }
+    }
+  }
+  if (tested) *tested = cnt;
+  return bad;
 }

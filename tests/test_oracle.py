@@ -326,3 +326,18 @@ def test_kernel_traversal_opencl_semantics(hostsim, oracle, rtg, golden):
         assert bits_equal(got, want), first_mismatch(got, want)
     finally:
         hostsim.hostsim_set_variant(0)
+
+
+def test_overlap_masks_bound_containment(hostsim):
+    """A sphere left out of overlap mask h never contains the refraction test
+    point P + 0.01f D of a hit point P in h's guard ball with |D| <= 3, by
+    the reference's own containment test (raytracer.h:255-264), over random
+    scenes at scales 0.03..30 with half of the spheres placed just outside the
+    reach (relative gaps 1e-5..1e-2), negative radii included."""
+    f = hostsim.hostsim_contain_mask_check
+    f.restype = ctypes.c_long
+    tested = ctypes.c_long(0)
+    bad = f(ctypes.c_long(300), 12, ctypes.c_long(80), ctypes.c_ulonglong(7),
+            ctypes.byref(tested))
+    assert bad == 0, bad
+    assert tested.value > 200_000, tested.value
