@@ -57,8 +57,81 @@ RTG_HD V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RTG_HD V3 vmul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 RTG_HD V3 vsmul(float k, V3 b) { return v3(k * b.x, k * b.y, k * b.z); }
 RTG_HD float vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-RTG_HD float rtg_sqrtf(float x) { return sqrtf(x); }
-RTG_HD V3 vnorm(V3 v) { float l = 1.f / rtg_sqrtf(vdot(v, v)); return vsmul(l, v); }
+// Correctly rounded square root and reciprocal, bit-identical to sqrtf(x)
+// and 1.f / b (IEEE binary32, round to nearest), with a short sequence for
+// the operand range the traversal meets and the compiler's full sequence for
+// the rest (per lane; the wave skips it when no lane needs it).
+//  * sqrt_rn, x in [2^-96, FLT_MAX]: s = v_sqrt_f32(x) (within 1 ulp), then
+//    the neighbour s -+ 1 ulp whose residual fma(-s', s, x) shows that it is
+//    the rounded root (the residuals are exact fused products; no scaling is
+//    needed above 2^-96).  9 VALU instead of ~17 (the compiler's expansion
+//    scales small operands and patches 0/inf with a class test).
+//  * rcp_rn, b in [2^-125, 2^125]: y = v_rcp_f32(b), one Newton step
+//    y + y (1 - b y) with fused operations (Markstein).  3 VALU instead of
+//    the ~11 of a general division.
+// tests/fpcheck/fpcheck_gpu.hip checks both against sqrtf / 1.f / b and
+// against an exact (f64) rounding criterion for EVERY float in those ranges
+// on the GPU (test_gpu_parity.py::test_fast_sqrt_rcp_exhaustive).
+RTG_HD bool sqrt_fast_range(float x) {
+  unsigned u;
+  memcpy(&u, &x, 4);
+  return u - 0x0F800000u <= 0x7F7FFFFFu - 0x0F800000u;  // 2^-96 <= x <= FLT_MAX
+}
+RTG_HD bool rcp_fast_range(float b) {
+  unsigned u;
+  memcpy(&u, &b, 4);
+  return u - 0x01000000u <= 0x7E000000u - 0x01000000u;  // 2^-125 <= b <= 2^125
+}
+RTG_HD float sqrt_fast(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+  const float su = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rd = fmaf(-sd, s, x);
+  const float ru = fmaf(-su, s, x);
+  s = (rd <= 0.f) ? sd : s;
+  s = (ru > 0.f) ? su : s;
+  return s;
+#else
+  return sqrtf(x);
+#endif
+}
+RTG_HD float rcp_fast(float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float y = __builtin_amdgcn_rcpf(b);
+  const float e = fmaf(-b, y, 1.0f);
+  return fmaf(e, y, y);
+#else
+  return 1.f / b;
+#endif
+}
+// The fallback stays a branch the wave skips when no lane needs it: the
+// empty volatile asm keeps the compiler from speculating the (one-IR-op,
+// long-expansion) sqrtf / fdiv into a select next to the short sequence.
+RTG_HD void no_speculate() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("");
+#endif
+}
+RTG_HD float sqrt_rn(float x) {
+  float s = sqrt_fast(x);
+  if (!sqrt_fast_range(x)) {
+    no_speculate();
+    s = sqrtf(x);
+  }
+  return s;
+}
+RTG_HD float rcp_rn(float b) {
+  float y = rcp_fast(b);
+  if (!rcp_fast_range(b)) {
+    no_speculate();
+    y = 1.f / b;
+  }
+  return y;
+}
+RTG_HD float rtg_sqrtf(float x) { return sqrt_rn(x); }
+// vec.h:41: l = 1.f / sqrt(dot); v *= l.
+RTG_HD V3 vnorm(V3 v) { float l = rcp_rn(rtg_sqrtf(vdot(v, v))); return vsmul(l, v); }
 // raytracer.h:235-241
 RTG_HD bool significant(V3 c) { return (c.x >= 0.001f) || (c.y >= 0.001f) || (c.z >= 0.001f); }
 
@@ -130,7 +203,7 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.den = 2.0f * a;
   q.ap = a * (1.0f - 0x1p-16f);
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
-  q.y = 1.0f / q.den;
+  q.y = rcp_rn(q.den);
   return q;
 }
 
@@ -279,7 +352,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
     sc.light(l, Lpos, Lcol);
     V3 dist = vsub(Lpos, P);
     const float gap = vdot(dist, dist);
-    const V3 dir = vsmul(1.f / rtg_sqrtf(gap), dist);  // vnorm(dist)
+    const V3 dir = vsmul(rcp_rn(rtg_sqrtf(gap)), dist);  // vnorm(dist)
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
       sc.probe_begin(kProbeShadow);
@@ -357,7 +430,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   if (wantRay) {
     // solveQuadratic(1, 2cosA1, 1 - 1/ratio^2), algebra.h:22-65 with a = 1.
     const float qb = 2.f * cosA1;
-    const float qc = 1.f - (1.f / (ratio * ratio));
+    const float qc = 1.f - rcp_rn(ratio * ratio);
     const float rad = (qb * qb) - ((4.f * 1.f) * qc);
     float r0, r1;
     int ns;

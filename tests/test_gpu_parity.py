@@ -473,3 +473,21 @@ def test_host_driver_opencl_semantics_ppm(R, oracle, tmp_path):
     sph, lg = R.reference_scene()
     want = R.ppm_file_bytes(oracle.render_cl(sph, lg, 200, 150, 5))
     assert open(out, "rb").read() == want
+
+
+def test_fast_sqrt_rcp_exhaustive():
+    """rtg_trace.h's short sequences for the correctly rounded square root and
+    reciprocal (sqrt_rn / rcp_rn, used by every vnorm and every query's 1/2a)
+    against the compiler's correctly rounded sqrtf and 1.f / x, and against an
+    exact f64 rounding criterion, for EVERY binary32 bit pattern, on the GPU
+    (tests/fpcheck/fpcheck_gpu.hip)."""
+    so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fpcheck", "libfpcheck_gpu.so")
+    L = ctypes.CDLL(so)
+    out = (ctypes.c_ulonglong * 8)()
+    assert L.fpcheck_run(ctypes.c_ulonglong(0), out) == 0
+    sqrt_in, sqrt_lib, sqrt_exact, sqrt_all, rcp_in, rcp_lib, rcp_exact, rcp_all = list(out)
+    # the fast ranges: [2^-96, FLT_MAX] and [2^-125, 2^125]
+    assert sqrt_in == 0x7F7FFFFF - 0x0F800000 + 1
+    assert rcp_in == 0x7E000000 - 0x01000000 + 1
+    assert (sqrt_lib, sqrt_exact, sqrt_all) == (0, 0, 0), list(out)
+    assert (rcp_lib, rcp_exact, rcp_all) == (0, 0, 0), list(out)
