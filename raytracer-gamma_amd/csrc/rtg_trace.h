@@ -146,6 +146,11 @@ struct Camera {
 struct Mat { V3 matte, gloss; float opacity, refr; };
 
 // Diagnostic probe slots (scenes without probes implement them as no-ops).
+// Operation counters (host simulation only; sc.count is a no-op on the GPU).
+enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, kCntEnterOK,
+             kCntFullQ, kCntFullCand, kCntShadowQ, kCntShadowSel, kCntShadowCand,
+             kCntContainMasked, kCntContainSel, kCntContainFull, kCntRefraction, kCntReflPush,
+             kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
@@ -358,10 +363,14 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
       sc.probe_begin(kProbeShadow);
       bool blk;
       if constexpr (Q == 4) {
-        if (sc.has_smask())
-          blk = blocked_sel(sc, P, dir, gap, sc.shadow_union(l, hit, guardOK));
-        else
+        if (sc.has_smask()) {
+          const uint64_t su = sc.shadow_union(l, hit, guardOK);
+          sc.count(kCntShadowQ, 1);
+          sc.count(kCntShadowSel, __builtin_popcountll(su));
+          blk = blocked_sel(sc, P, dir, gap, su);
+        } else {
           blk = query_blocked<2>(sc, P, dir, gap);
+        }
       } else {
         blk = query_blocked<Q>(sc, P, dir, gap);
       }
@@ -418,8 +427,12 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   int tgt;
   if (hit >= 0 && sc.has_smask()) {
     const bool ok = guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax;
-    tgt = primary_container_sel(sc, testPt, sc.contain_union(hit, ok));
+    const uint64_t cu = sc.contain_union(hit, ok);
+    sc.count(kCntContainMasked, 1);
+    sc.count(kCntContainSel, __builtin_popcountll(cu));
+    tgt = primary_container_sel(sc, testPt, cu);
   } else {
+    sc.count(kCntContainFull, 1);
     tgt = primary_container(sc, testPt);
   }
   if (tgt < 0) tgt = (int)sc.n;  // background material
@@ -489,14 +502,19 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     sc.probe_begin(kProbeClosest);
     int hit;
     if (usePrim) {  // the primary ray: only spheres its wave's bundle can reach
+      sc.count(kCntPrimQ, 1);
+      sc.count(kCntPrimSel, __builtin_popcountll(primSel));
       hit = closest_hit_sel(sc, o, d, t, primSel);
       usePrim = false;
     } else if (Q == 4 && sc.has_smask() && sc.all(enterH >= 0)) {
       // every active lane traces a ray that entered a sphere: try h + overlaps
       bool ok;
       hit = closest_enter(sc, make_query(o, d), enterH, t, ok);
+      sc.count(kCntEnterQ, 1);
+      sc.count(kCntEnterOK, ok ? 1 : 0);
       if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
     } else {
+      sc.count(kCntFullQ, 1);
       hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
     }
     enterH = -1;
@@ -533,6 +551,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         V3 cdir;
         float R;
         sc.probe_begin(kProbeRefraction);
+        sc.count(kCntRefraction, 1);
         const int tgt = Q == 4 ? refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R, hit, guardOK)
                                : refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R);
         sc.probe_end(kProbeRefraction);
@@ -549,6 +568,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           f.cx = colour.x; f.cy = colour.y; f.cz = colour.z;
           f.meta = ((unsigned)rm << 2) | (sigR ? 2u : 0u);
           if (sigR) {
+            sc.count(kCntReflPush, 1);
             // calculateReflection, raytracer.h:817-842
             const float perp = 2.f * vdot(d, N);
             const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
@@ -750,6 +770,7 @@ RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
+      sc.count(kCntFullCand, 1);
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;
@@ -812,6 +833,7 @@ RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
     while (cand) {
       const unsigned i = base + (unsigned)lowest_bit(cand);
       cand &= cand - 1;
+      sc.count(kCntShadowCand, 1);
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;
@@ -890,6 +912,7 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
   while (cand) {
     const unsigned i = (unsigned)__builtin_ctzll(cand);
     cand &= cand - 1;
+    sc.count(kCntPrimCand, 1);
     float r2;
     const V3 c = sc.sphere_lane(i, r2);
     bool res;

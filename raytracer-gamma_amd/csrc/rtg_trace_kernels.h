@@ -71,6 +71,7 @@ struct DevScene {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  __device__ __forceinline__ void count(int, long) const {}  // host simulation only
   cfloat_p geom;      // n x {x, y, z, r*r}
   cfloat_p crad2;
   MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)

@@ -17,8 +17,11 @@
 void rtg_set_error(const char*, ...) {}
 void rtg_clear_error() {}
 
+long g_counts[rtg::kCntSlots];
+
 namespace {
 struct HostScene {
+  void count(int slot, long v) const { g_counts[slot] += v; }
   const float* geom;
   const float* crad2;
   const float* mats;
@@ -108,6 +111,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
                                         : rtg::trace_sample<S, 4>(sc, d, sc.frames());
           c = rtg::vsmul(cam.inv, c);
           p = rtg::vadd(p, c);
+          g_counts[rtg::kCntSamples] += 1;
         }
         break;
       }
@@ -139,6 +143,15 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 }  // namespace
 
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
+// Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
+// the renders since the last reset (diagnostic; single-lane semantics, so the
+// wave unions of the GPU are per-sample masks here).
+extern "C" void hostsim_counts(long* out, int reset) {
+  for (int k = 0; k < rtg::kCntSlots; ++k) {
+    out[k] = g_counts[k];
+    if (reset) g_counts[k] = 0;
+  }
+}
 
 extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
                                    const rtg_light* lights, unsigned m, unsigned W,
