@@ -95,9 +95,9 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
     out[i] = ppm_byte(c[i], m);
 }
 
-static TraceFn pick_trace(int S, bool lds, int variant) {
+static TraceFn pick_trace(int S, bool lds, int variant, bool bvh) {
   switch (S) {
-#define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant);
+#define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant, bvh);
     RTG_CASE(1) RTG_CASE(2) RTG_CASE(3) RTG_CASE(4) RTG_CASE(5) RTG_CASE(6) RTG_CASE(7)
     RTG_CASE(8) RTG_CASE(9) RTG_CASE(10) RTG_CASE(11) RTG_CASE(12) RTG_CASE(13)
     RTG_CASE(14) RTG_CASE(15) RTG_CASE(16)
@@ -116,6 +116,9 @@ struct rtg_context {
   float* mats = nullptr;
   float* lights = nullptr;
   unsigned* smask = nullptr;  // shadow masks (null when the scene has none)
+  float* bvhNodes = nullptr;  // BVH (null when the scene has none)
+  float* bvhAux = nullptr;
+  int* bvhChild = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
@@ -133,7 +136,13 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->mats);
   (void)hipFree(c->lights);
   (void)hipFree(c->smask);
+  (void)hipFree(c->bvhNodes);
+  (void)hipFree(c->bvhAux);
+  (void)hipFree(c->bvhChild);
   c->smask = nullptr;
+  c->bvhNodes = nullptr;
+  c->bvhAux = nullptr;
+  c->bvhChild = nullptr;
   c->geom = nullptr;
   c->crad2 = nullptr;
   c->mats = nullptr;
@@ -324,6 +333,21 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->smask, ps.smask.data(), ps.smask.size() * sizeof(unsigned),
                       hipMemcpyHostToDevice));
   }
+  if (!ps.bvhChild.empty()) {
+    if (hipMalloc(&ctx->bvhNodes, ps.bvhNodes.size() * sizeof(float)) != hipSuccess ||
+        hipMalloc(&ctx->bvhAux, ps.bvhAux.size() * sizeof(float)) != hipSuccess ||
+        hipMalloc(&ctx->bvhChild, ps.bvhChild.size() * sizeof(int)) != hipSuccess) {
+      free_scene(ctx);
+      rtg_set_error("hipMalloc failed for the BVH");
+      return RTG_ERR_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(ctx->bvhNodes, ps.bvhNodes.data(), ps.bvhNodes.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->bvhAux, ps.bvhAux.data(), ps.bvhAux.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->bvhChild, ps.bvhChild.data(), ps.bvhChild.size() * sizeof(int),
+                      hipMemcpyHostToDevice));
+  }
   ctx->n = sphNum;
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
@@ -362,7 +386,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 50 ||
       variant == 110)
     ldsMats = false;
-  TraceFn fn = pick_trace(stackSize, ldsMats, variant);
+  TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr);
   if (!fn) {
     rtg_set_error("no kernel for stackSize %d (valid: 1..%d), variant %d", stackSize,
                   RTG_MAX_STACK, variant);
@@ -388,6 +412,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.mats = ctx->mats;
   a.lights = ctx->lights;
   a.smask = ctx->smask;
+  a.bvhNodes = ctx->bvhNodes;
+  a.bvhAux = ctx->bvhAux;
+  a.bvhChild = ctx->bvhChild;
   a.n = ctx->n;
   a.m = ctx->m;
   a.n4 = ctx->n4;
@@ -422,9 +449,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     grid = dim3((unsigned)blocks, 1);
   }
   const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * threads * 16;
-  const size_t lds = frameLds + (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) +
-                                            (size_t)ctx->n4 * 16)
-                                         : 0);
+  const size_t lds = frameLds +
+                     (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) + (size_t)ctx->n4 * 16)
+                              : 0) +
+                     (ctx->bvhNodes ? (size_t)(threads / 64) * 64 * sizeof(int) : 0);
   if (ctx->opts.flags & RTG_LAUNCH_TIMELINE) {
     const size_t waves = (size_t)grid.x * grid.y * (threads / 64);
     if (ctx->timelineCap < waves) {

@@ -14,6 +14,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
+#include <functional>
 #include <vector>
 
 #include "rtg.h"
@@ -21,6 +23,9 @@
 #include "rtg_trace.h"
 
 namespace rtg {
+
+// Scenes above this many spheres have no masks; they get a BVH instead.
+constexpr unsigned kMaskMaxSpheres = 64;
 
 // Device image of a scene (crad2's third segment, guard_r2, and smask are
 // the shadow-ray masks' data, see shadow_masks).  geom: n x {x, y, z, r*r} followed by NaN padding
@@ -38,6 +43,13 @@ struct PackedScene {
   // masks, each {lo, hi} words, for 1 <= n <= 64 and a finite scene; empty
   // otherwise (every sphere is then tested).
   std::vector<unsigned> smask;
+  // BVH of scenes above kMaskMaxSpheres spheres (build_bvh): per node 4
+  // slots {x, y, z, screen radius^2} (bound_r2 for a child node, screen_r2
+  // for a sphere), 4 children (> 0 node, < 0 ~sphere index, 0 empty) and 4
+  // {prune radius, containment radius^2}; empty for small or non-finite
+  // scenes.
+  std::vector<float> bvhNodes, bvhAux;
+  std::vector<int> bvhChild;
   unsigned n = 0, m = 0;
   unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records
 };
@@ -97,7 +109,7 @@ inline double contain_reach(const rtg_sphere& s) {
 inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                          unsigned m, std::vector<unsigned>* out) {
   out->clear();
-  if (n == 0 || n > 64) return;
+  if (n == 0 || n > kMaskMaxSpheres) return;
   auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
   for (unsigned i = 0; i < n; ++i)
     if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
@@ -178,6 +190,143 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
   }
 }
 
+// 4-wide BVH of bounding spheres (the queries are closest_bvh, blocked_bvh
+// and container_bvh in rtg_trace.h).  Top-down: a node's spheres are split at
+// the median of the longest centroid axis, and each half again, into four
+// groups; a group of one sphere becomes a sphere slot, a larger group a child
+// node; nodes of <= 4 spheres hold sphere slots only.  Bounds are computed in
+// double about the float-rounded centre C of the group's box:
+//   R  = max |c_i - C| + |r_i|            (screen: bound_r2(R (1 + 2^-20)))
+//   RC = (max |c_i - C| + |r_i| + 1e-6) (1 + 2^-16)   (containment, RC^2 up)
+//   prune radius R (1 + 2^-7), rounded up (|r_i| (1 + 2^-7) for a sphere
+//   slot; see beyond_t in rtg_trace.h).
+// Returns false (no BVH) for non-finite scenes or an implausibly deep tree.
+inline float round_up_f(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, __builtin_inff());
+  return f;
+}
+
+inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
+  ps->bvhNodes.clear();
+  ps->bvhAux.clear();
+  ps->bvhChild.clear();
+  if (n <= kMaskMaxSpheres) return false;
+  auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
+  for (unsigned i = 0; i < n; ++i)
+    if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
+        !finite(spheres[i].radius))
+      return false;
+  std::vector<unsigned> idx(n);
+  for (unsigned i = 0; i < n; ++i) idx[i] = i;
+  auto cen = [&](unsigned i, int ax) {
+    return ax == 0 ? (double)spheres[i].pos.x : ax == 1 ? (double)spheres[i].pos.y
+                                                        : (double)spheres[i].pos.z;
+  };
+  auto longest = [&](unsigned lo, unsigned hi) {
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    for (unsigned k = lo; k < hi; ++k)
+      for (int a = 0; a < 3; ++a) {
+        mn[a] = fmin(mn[a], cen(idx[k], a));
+        mx[a] = fmax(mx[a], cen(idx[k], a));
+      }
+    int ax = 0;
+    for (int a = 1; a < 3; ++a)
+      if (mx[a] - mn[a] > mx[ax] - mn[ax]) ax = a;
+    return ax;
+  };
+  auto split = [&](unsigned lo, unsigned hi) {  // median split of idx[lo, hi)
+    const int ax = longest(lo, hi);
+    const unsigned mid = lo + (hi - lo) / 2;
+    std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi,
+                     [&](unsigned a, unsigned b) {
+                       const double ca = cen(a, ax), cb = cen(b, ax);
+                       return ca < cb || (ca == cb && a < b);
+                     });
+    return mid;
+  };
+  // bound of idx[lo, hi): C (float), R, RC (double)
+  auto bound = [&](unsigned lo, unsigned hi, float C[3], double& R, double& RC) {
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+    for (unsigned k = lo; k < hi; ++k) {
+      const rtg_sphere& s = spheres[idx[k]];
+      const double r = fabs((double)s.radius);
+      for (int a = 0; a < 3; ++a) {
+        mn[a] = fmin(mn[a], cen(idx[k], a) - r);
+        mx[a] = fmax(mx[a], cen(idx[k], a) + r);
+      }
+    }
+    for (int a = 0; a < 3; ++a) C[a] = (float)(0.5 * (mn[a] + mx[a]));
+    R = 0.0;
+    for (unsigned k = lo; k < hi; ++k) {
+      const rtg_sphere& s = spheres[idx[k]];
+      const double dx = cen(idx[k], 0) - C[0], dy = cen(idx[k], 1) - C[1],
+                   dz = cen(idx[k], 2) - C[2];
+      R = fmax(R, sqrt(dx * dx + dy * dy + dz * dz) + fabs((double)s.radius));
+    }
+    RC = (R + 1e-6) * (1.0 + 0x1p-16);
+  };
+  int maxDepth = 0;
+  // node for idx[lo, hi), returns its index
+  std::function<int(unsigned, unsigned, int)> build = [&](unsigned lo, unsigned hi,
+                                                          int depth) -> int {
+    maxDepth = depth > maxDepth ? depth : maxDepth;
+    const int node = (int)(ps->bvhChild.size() / 4);
+    ps->bvhNodes.resize(ps->bvhNodes.size() + 16, __builtin_nanf(""));
+    ps->bvhAux.resize(ps->bvhAux.size() + 8, -1.f);
+    ps->bvhChild.resize(ps->bvhChild.size() + 4, 0);
+    unsigned g[5];
+    const unsigned cnt = hi - lo;
+    if (cnt <= 4) {
+      for (unsigned k = 0; k <= cnt; ++k) g[k] = lo + k;
+      for (unsigned k = cnt + 1; k <= 4; ++k) g[k] = hi;
+    } else {
+      g[0] = lo;
+      g[4] = hi;
+      g[2] = split(lo, hi);
+      g[1] = split(lo, g[2]);
+      g[3] = split(g[2], hi);
+    }
+    for (int k = 0; k < 4; ++k) {
+      const unsigned a = g[k], b = g[k + 1];
+      if (a >= b) continue;
+      int child;
+      float C[3], w, cr, rp;
+      if (b - a == 1) {
+        const unsigned i = idx[a];
+        const rtg_sphere& s = spheres[i];
+        C[0] = s.pos.x; C[1] = s.pos.y; C[2] = s.pos.z;
+        w = screen_r2(s.radius * s.radius);
+        const float rc = s.radius + 1.0e-6f;
+        cr = rc * rc;
+        rp = round_up_f(fabs((double)s.radius) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
+        child = ~(int)i;
+      } else {
+        double R, RC;
+        bound(a, b, C, R, RC);
+        w = bound_r2(R * (1.0 + 0x1p-20));
+        cr = round_up_f(RC * RC);
+        rp = round_up_f(R * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
+        child = build(a, b, depth + 1);
+      }
+      float* rec = &ps->bvhNodes[(size_t)node * 16 + 4 * k];
+      rec[0] = C[0]; rec[1] = C[1]; rec[2] = C[2]; rec[3] = w;
+      ps->bvhAux[(size_t)node * 8 + 2 * k] = rp;
+      ps->bvhAux[(size_t)node * 8 + 2 * k + 1] = cr;
+      ps->bvhChild[(size_t)node * 4 + k] = child;
+    }
+    return node;
+  };
+  build(0, n, 0);
+  if (maxDepth > 20) {  // the wave stack holds 3 * depth + 1 <= 64 entries
+    ps->bvhNodes.clear();
+    ps->bvhAux.clear();
+    ps->bvhChild.clear();
+    return false;
+  }
+  return true;
+}
+
 inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                        unsigned m, PackedScene* ps) {
   ps->n = n;
@@ -212,6 +361,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   }
   ps->mats[(size_t)n * 8 + 7] = 1.00f;
   shadow_masks(spheres, n, lights, m, &ps->smask);
+  build_bvh(spheres, n, ps);
   for (unsigned l = 0; l < m; ++l) {
     float* p = &ps->lights[(size_t)l * 6];
     p[0] = lights[l].pos.x; p[1] = lights[l].pos.y; p[2] = lights[l].pos.z;

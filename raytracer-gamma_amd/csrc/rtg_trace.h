@@ -150,7 +150,7 @@ struct Mat { V3 matte, gloss; float opacity, refr; };
 enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, kCntEnterOK,
              kCntFullQ, kCntFullCand, kCntShadowQ, kCntShadowSel, kCntShadowCand,
              kCntContainMasked, kCntContainSel, kCntContainFull, kCntRefraction, kCntReflPush,
-             kCntSlots };
+             kCntBvhNodeTests, kCntBvhSphereTests, kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
@@ -192,10 +192,14 @@ struct Frame {
 // property over 1e9 operand pairs (incl. subnormal numerators and values at
 // both thresholds) for den in [2^-60, 2^60].  Outside that range the correctly
 // rounded division is used.
+// Slack of the BVH node screens (bound_r2, rtg_scene_pack.h build_bvh).
+constexpr float kBoundK = 0x1p-7f;
+
 struct RayQ {
   V3 o, d;
   float a4, den, y;
   float ap;       // pass-1 screen: a (1 - K), K = 2^-16 (pass1_rad)
+  float apB;      // BVH bound screen: a (1 - K_B), K_B = kBoundK (bound_r2)
   bool fast;
 };
 
@@ -207,6 +211,7 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.a4 = 4.0f * a;
   q.den = 2.0f * a;
   q.ap = a * (1.0f - 0x1p-16f);
+  q.apB = a * (1.0f - kBoundK);
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
   q.y = rcp_rn(q.den);
   return q;
@@ -292,7 +297,11 @@ RTG_HD int lowest_bit(unsigned m) {
 // past n never matches); the first index is the lowest set bit, and the wave
 // stops once every lane has its answer.
 template <class Scene>
+RTG_HD int container_bvh(const Scene& sc, V3 pt);
+
+template <class Scene>
 RTG_HD int primary_container(const Scene& sc, V3 pt) {
+  if (sc.has_bvh()) return container_bvh(sc, pt);
   int found = -1;
   const unsigned n4 = sc.n4;
   for (unsigned k = 0; k < n4; k += 4) {  // wave-uniform
@@ -741,6 +750,236 @@ inline float screen_r2(float r2) {
   return f;
 }
 
+// ---------------------------------------------------------------------------
+// BVH queries for scenes above 64 spheres (no shadow/overlap masks there).
+// The host builds a 4-wide tree of bounding spheres (build_bvh,
+// rtg_scene_pack.h); the wave walks it together: a node's child is visited
+// when the child's bound screen passes for ANY active lane (ballot), so node
+// indices, records and the stack stay wave-uniform (scalar loads, the stack
+// in one VGPR through v_writelane / v_readlane).  Leaf spheres get the
+// pass-1 screen and the reference's exact root test per lane.  The queries
+// take the same answers as the flat ones whatever order the tree visits
+// spheres in:
+//  * closest hit (raytracer.h:145-194: index order, strict <, minT from
+//    1000) = the lexicographic minimum of (t, i) over accepted roots t < 1000;
+//  * shadow (raytracer.h:272-309) = does ANY accepted root block;
+//  * container (raytracer.h:245-270) = the minimum index whose containment
+//    test passes.
+// A node bound (C, R) holds every member sphere (R >= |c_i - C| + |r_i|); its
+// screen is pass1_rad's with slack K_B = kBoundK instead of K: a line the
+// reference accepts for member i passes within R + sqrt(E/a) of C, E ~ 10 eps
+// a (|p_i|^2 + r_i^2) being the reference radicand's rounding error, so the
+// bound's true radicand/4 is >= -2 sqrt(30 eps) a (|p_B|^2 + R^2) ~ -2^-8.5
+// a (...), which K_B = 2^-7 covers with room for the screen's own rounding
+// (tests/test_oracle.py::test_bvh_bound_screen_is_a_superset).
+RTG_HD float pass1_bound(const RayQ& q, V3 c, float rsB) {
+  const V3 p = vsub(q.o, c);
+  const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+  const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rsB)));
+  return fmaf(x, x, fmaf(-q.apB, cs, 0x1p-100f));
+}
+
+// Bound screen radius^2: R^2 (1 + 2 K_B + 4 K_B^2) >= R^2 (1 + K_B) / (1 - K_B),
+// R given in double, rounded up to float.
+inline float bound_r2(double R) {
+  const double K = (double)kBoundK;
+  const double v = R * R * (1.0 + 2.0 * K + 4.0 * K * K);
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, __builtin_inff());
+  return f;
+}
+
+// Wave-uniform traversal stack: 64 entries of the wave's LDS area
+// (sc.bvh_stack()).  Every active lane writes the same entry and reads it
+// back (LDS accesses of one wave complete in order); the popped index is made
+// scalar with v_readfirstlane.  (A stack in the lanes of a VGPR does not
+// survive the divergent callers: copies of a VGPR only move active lanes.)
+struct BvhStack {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int* v;
+  unsigned sp = 0;
+  __device__ __forceinline__ explicit BvhStack(int* lds) : v(lds) {}
+  __device__ __forceinline__ void push(int x) {  // x, sp wave-uniform
+    v[sp] = x;
+    ++sp;
+  }
+  __device__ __forceinline__ int pop() {
+    --sp;
+    return __builtin_amdgcn_readfirstlane(v[sp]);
+  }
+#else
+  int v[64];
+  unsigned sp = 0;
+  explicit BvhStack(int*) {}
+  void push(int x) { v[sp++] = x; }
+  int pop() { return v[--sp]; }
+#endif
+  RTG_HD bool empty() const { return sp == 0; }
+};
+
+// Distance pruning.  An accepted root t of sphere i (raytracer.h:105-138)
+// lies on the ray no nearer than |p_i| - r_i - mu_i with mu_i = 2^-8 (|p_i| +
+// r_i) (p_i = o - c_i; the same root-error bound as shadow_masks': roots
+// move by ~sqrt(14 eps)(|p| + r) near tangency), i.e. t |d| >= |p_i| - r_i -
+// mu_i; for a node bound (C, R) holding sphere i, |p_i| - r_i >= |p_B| - R
+// and mu_i <= 2^-8 (|p_B| + 2 R).  So with rp >= R (1 + 2^-7) (the slot's
+// prune radius) every member's accepted roots are beyond `reach` when
+//   |p_B| (1 - 2^-8) > rp + reach,
+// tested squared with p2 = |p_B|^2 (relative rounding below 2^-20 on both
+// sides, covered by the two factors).  `reach` is minT |d|_up for a closest
+// query (a root must be < minT, or == minT with a lower index, to win) and
+// sqrt(gap)_up for a shadow ray (|t D|^2 < gap to block).
+// tests/test_oracle.py::test_bvh_root_distance_bound checks the root bound
+// on adversarial rays.
+RTG_HD bool beyond(float p2, float rp, float reach) {
+  const float s = rp + reach;
+  return p2 * (0x1.fc02p-1f * (1.0f - 0x1p-18f)) > s * s * (1.0f + 0x1p-18f);
+}
+// |d| rounded up (v_sqrt_f32 is within 1 ulp).
+RTG_HD float norm_up(float a) { return sqrtf(a) * (1.0f + 0x1p-20f); }
+
+// Children of a node in front-to-back order for the wave: pushes the valid
+// (child, key) pairs, keys = a lane's |p_B|^2 (wave-uniform), farthest first
+// so that the nearest is popped next.  Five compare-exchanges.
+RTG_HD void push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2, float k2,
+                        int c3, float k3) {
+  auto cx = [](int& ca, float& ka, int& cb, float& kb) {
+    if (kb > ka) {
+      const int ct = ca; ca = cb; cb = ct;
+      const float kt = ka; ka = kb; kb = kt;
+    }
+  };
+  cx(c0, k0, c1, k1);
+  cx(c2, k2, c3, k3);
+  cx(c0, k0, c2, k2);
+  cx(c1, k1, c3, k3);
+  cx(c1, k1, c2, k2);
+  if (c0 > 0) st.push(c0);
+  if (c1 > 0) st.push(c1);
+  if (c2 > 0) st.push(c2);
+  if (c3 > 0) st.push(c3);
+}
+
+// One node of a ray query: bound screens and distance pruning of its four
+// slots; child nodes some active lane still needs are pushed front to back,
+// sphere slots are handed to `leaf(i, c)` for lanes that pass the screen and
+// the prune.  `active`: the lane still queries; `reach`: its pruning reach.
+template <class Scene, class Leaf>
+RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active, float reach,
+                         BvhStack& st, Leaf&& leaf) {
+  V3 c[4];
+  float w[4], rp[4], cr[4];
+  int ch[4];
+  sc.bvh_node(nd, c, w, ch);
+  sc.bvh_aux(nd, rp, cr);
+  int pc[4];
+  float pk[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    pc[k] = 0;
+    pk[k] = 0.f;
+    const int x = ch[k];
+    if (x == 0) continue;  // wave-uniform
+    const V3 p = vsub(q.o, c[k]);
+    const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+    const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
+    const bool near = !beyond(p2, rp[k], reach);
+    if (x > 0) {
+      sc.count(kCntBvhNodeTests, 1);
+      const float v = fmaf(xd, xd, fmaf(-q.apB, p2 - w[k], 0x1p-100f));  // pass1_bound
+      if (sc.any(active && near && !(v < 0.f))) {
+        pc[k] = x;
+        pk[k] = sc.first_lane(p2);
+      }
+    } else {
+      sc.count(kCntBvhSphereTests, 1);
+      const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - w[k], 0x1p-100f));  // pass1_rad
+      if (active && near && !(v < 0.f)) leaf((unsigned)~x);
+    }
+  }
+  push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
+}
+
+template <class Scene>
+RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
+  float minT = 1000.f;
+  int best = -1;
+  const float dn = norm_up(q.den * 0.5f);
+  BvhStack st(sc.bvh_stack());
+  st.push(0);
+  while (!st.empty()) {  // wave-uniform
+    const unsigned nd = (unsigned)st.pop();
+    bvh_ray_node(sc, q, nd, true, minT * dn, st, [&](unsigned i) {
+      sc.count(kCntFullCand, 1);
+      float r2;
+      const V3 ce = sc.sphere(i, r2);
+      bool res;
+      const float t = ray_sphere(q, ce, r2, res);
+      if (res && (t < minT || (t == minT && (int)i < best))) {
+        minT = t;
+        best = (int)i;
+      }
+    });
+  }
+  tOut = minT;
+  return best;
+}
+
+template <class Scene>
+RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
+  bool blk = false;
+  const float reach = norm_up(gap);
+  BvhStack st(sc.bvh_stack());
+  st.push(0);
+  while (!st.empty()) {  // wave-uniform
+    if (sc.all(blk)) break;
+    const unsigned nd = (unsigned)st.pop();
+    bvh_ray_node(sc, q, nd, !blk, reach, st, [&](unsigned i) {
+      sc.count(kCntShadowCand, 1);
+      float r2;
+      const V3 ce = sc.sphere(i, r2);
+      bool res;
+      const float t = ray_sphere(q, ce, r2, res);
+      if (res && t < 1000.f) {
+        const V3 dist = vsmul(t, q.d);
+        if (vdot(dist, dist) < gap) blk = true;
+      }
+    });
+  }
+  return blk;
+}
+
+// Node bounds for containment: |pt - C|^2 <= RC^2 with RC >= |c_i - C| +
+// |r_i| + 1e-6 and a relative 2^-16 margin (the reference's test accepts at
+// most a few ulps outside (r_i + 1e-6)); leaf slots hold (r_i + 1e-6f)^2.
+template <class Scene>
+RTG_HD int container_bvh(const Scene& sc, V3 pt) {
+  int found = 0x7FFFFFFF;
+  BvhStack st(sc.bvh_stack());
+  st.push(0);
+  while (!st.empty()) {  // wave-uniform
+    const int nd = st.pop();
+    V3 c[4];
+    float w[4], rp[4], cr[4];
+    int ch[4];
+    sc.bvh_node((unsigned)nd, c, w, ch);
+    sc.bvh_aux((unsigned)nd, rp, cr);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = ch[k];
+      if (x == 0) continue;
+      const V3 dist = vsub(pt, c[k]);
+      const bool in = vdot(dist, dist) <= cr[k];
+      if (x > 0) {
+        if (sc.any(in)) st.push(x);
+      } else if (in && (int)~x < found) {
+        found = (int)~x;
+      }
+    }
+  }
+  return found == 0x7FFFFFFF ? -1 : found;
+}
+
 template <class Scene>
 RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, const RayQ& q) {
   // Groups of 4 from the last to the first, so sphere base + k lands in bit k;
@@ -761,6 +1000,7 @@ RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, con
 template <class Scene>
 RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
   const RayQ q = make_query(o, d);
+  if (sc.has_bvh()) return closest_bvh(sc, q, tOut);
   float minT = 1000.f;
   int best = -1;
   const unsigned n = sc.n;
@@ -786,6 +1026,7 @@ RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
 template <class Scene>
 RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
   const RayQ q = make_query(o, d);
+  if (sc.has_bvh()) return blocked_bvh(sc, q, gap);
   const unsigned n = sc.n;
   for (unsigned base = 0; base < n; base += 32) {
     const unsigned cnt = (n - base < 32u) ? (n - base) : 32u;

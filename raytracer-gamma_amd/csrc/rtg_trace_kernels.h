@@ -46,10 +46,13 @@ struct LdsFrames {
   __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kThreads]; }
 };
 
-template <class MatPtr, bool kDiag = false, int kThreads = kBlock>
+// kBvh: the kernel instantiation for BVH scenes (n > 64); without it the BVH
+// branches compile away, so small scenes keep the smaller, faster kernel.
+template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = false>
 struct DevScene {
   FrameC* lfr;
   __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
+  __device__ __forceinline__ bool any(bool b) const { return __ballot(b) != 0ull; }
   __device__ __forceinline__ LdsFrames<kThreads> frames() const {
     return LdsFrames<kThreads>{lfr};
   }
@@ -78,6 +81,10 @@ struct DevScene {
   const float4* lgeom;  // LDS copy of geom (or the global array when it does not fit)
   cfloat_p lights;
   cuint_p smask;  // m x n x {lo, hi} shadow masks, or null
+  cfloat_p bvhNodes;  // BVH (build_bvh, rtg_scene_pack.h) or null
+  int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
+  cfloat_p bvhAux;
+  const RTG_CONST int* bvhChild;
   unsigned n, m;
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
@@ -108,6 +115,35 @@ struct DevScene {
   }
   __device__ __forceinline__ V3 sphere_contain(unsigned i, float& cr) const {
     return sphere(2 * (n4 + 4) + i, cr);
+  }
+  // BVH node nd: four slots {centre, screen radius^2}, their children and
+  // containment radii^2 (wave-uniform nd: scalar loads).
+  __device__ __forceinline__ bool has_bvh() const {
+    if constexpr (kBvh) return bvhNodes != nullptr;
+    else return false;
+  }
+  __device__ __forceinline__ int* bvh_stack() const { return bvhStk; }
+  __device__ __forceinline__ void bvh_node(unsigned nd, V3* c, float* w, int* ch) const {
+    cfloat_p g = bvhNodes + 16 * nd;
+    const RTG_CONST int* h = bvhChild + 4 * nd;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
+      w[k] = g[4 * k + 3];
+      ch[k] = h[k];
+    }
+  }
+  __device__ __forceinline__ void bvh_aux(unsigned nd, float* rp, float* cr) const {
+    cfloat_p g = bvhAux + 8 * nd;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      rp[k] = g[2 * k];
+      cr[k] = g[2 * k + 1];
+    }
+  }
+  // One lane's value for wave-uniform decisions (traversal order only).
+  __device__ __forceinline__ float first_lane(float v) const {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
   }
   // Shadow and overlap masks (rtg_scene_pack.h shadow_masks): n <= 64.
   __device__ __forceinline__ bool has_smask() const { return smask != nullptr; }
@@ -174,6 +210,9 @@ struct KernelArgs {
   const float* mats;
   const float* lights;
   const unsigned* smask;  // shadow masks (PackedScene::smask) or null
+  const float* bvhNodes;  // BVH (PackedScene::bvh*) or null
+  const float* bvhAux;
+  const int* bvhChild;
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
@@ -224,6 +263,13 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.crad2 = (cfloat_p)a.crad2;
   sc.lights = (cfloat_p)a.lights;
   sc.smask = (cuint_p)a.smask;
+  sc.bvhNodes = (cfloat_p)a.bvhNodes;
+  // BVH scenes: 64 stack entries per wave after the frames and scene tables
+  // (the launcher adds them to the LDS size).
+  sc.bvhStk = reinterpret_cast<int*>(sceneLds + (kLds ? (a.n + 1) * 2 + a.n4 : 0)) +
+              (threadIdx.x >> 6) * 64;
+  sc.bvhAux = (cfloat_p)a.bvhAux;
+  sc.bvhChild = (const RTG_CONST int*)a.bvhChild;
   sc.n = a.n;
   sc.m = a.m;
   sc.n4 = a.n4;
@@ -312,7 +358,7 @@ __device__ __forceinline__ void record_wave(const KernelArgs& a, unsigned t0, si
 
 // Tile kernels: one 8 x 8 pixel tile per wave, all samples of a pixel in its
 // lane; a workgroup is 2 x 2 tiles.
-template <int S, bool kLds, int kVariant>
+template <int S, bool kLds, int kVariant, bool kBvh = false>
 __global__ __launch_bounds__(kBlock, (MinWaves<S, kVariant>::value))
 void trace_kernel(const KernelArgs a) {
   // LDS image: per-lane frame colours ((S-1) x threads x 16 B), then, when
@@ -320,7 +366,7 @@ void trace_kernel(const KernelArgs a) {
   constexpr int kThreads = kBlock;
   constexpr unsigned TW = 2u, TH = 2u;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100), kThreads> sc;
+  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh> sc;
   stage_scene<S, kLds, kThreads>(a, sc);
   const unsigned wave = threadIdx.x >> 6;
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
@@ -465,12 +511,12 @@ struct SampleThreads {
 
 // One launch, one pixel group per wave: one-wave workgroups (default), or
 // four-wave ones (variant 14).
-template <int S, bool kLds, int kVariant>
+template <int S, bool kLds, int kVariant, bool kBvh = false>
 __global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
 void trace_samples_kernel(const KernelArgs a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100), kThreads> sc;
+  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh> sc;
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
@@ -542,8 +588,26 @@ static TraceFn trace_fn_v(bool lds) {
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
 }
+// BVH scenes: the default kernels (and their diagnostic and OpenCL-semantics
+// forms) have kBvh instantiations; other A/B variants run BVH scenes through
+// their flat queries (same results, slower).
 template <int S>
-static TraceFn trace_fn(bool lds, int variant) {
+static TraceFn trace_fn_bvh(bool lds, int variant) {
+  switch (variant) {
+    case 0: return trace_samples_kernel<S, false, 0, true>;
+    case 50: return trace_samples_kernel<S, false, 50, true>;
+    case 110: return trace_samples_kernel<S, false, 110, true>;
+    case 9: return lds ? trace_kernel<S, true, 9, true> : trace_kernel<S, false, 9, true>;
+    case 59: return lds ? trace_kernel<S, true, 59, true> : trace_kernel<S, false, 59, true>;
+    case 100: return lds ? trace_kernel<S, true, 100, true> : trace_kernel<S, false, 100, true>;
+    default: return nullptr;
+  }
+}
+template <int S>
+static TraceFn trace_fn(bool lds, int variant, bool bvh) {
+  if (bvh) {
+    if (TraceFn f = trace_fn_bvh<S>(lds, variant)) return f;
+  }
   switch (variant) {
     case 100: return trace_fn_v<S, 100>(lds);
     case 110: return trace_fn_v<S, 110>(lds);
@@ -571,7 +635,7 @@ static TraceFn trace_fn(bool lds, int variant) {
 }
 
 // One per stack size, defined in rtg_trace_s<S>.hip.
-#define RTG_DECL(k) TraceFn trace_fn_s##k(bool lds, int variant);
+#define RTG_DECL(k) TraceFn trace_fn_s##k(bool lds, int variant, bool bvh);
 RTG_DECL(1) RTG_DECL(2) RTG_DECL(3) RTG_DECL(4) RTG_DECL(5) RTG_DECL(6) RTG_DECL(7)
 RTG_DECL(8) RTG_DECL(9) RTG_DECL(10) RTG_DECL(11) RTG_DECL(12) RTG_DECL(13)
 RTG_DECL(14) RTG_DECL(15) RTG_DECL(16)

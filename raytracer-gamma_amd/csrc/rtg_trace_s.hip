@@ -9,5 +9,7 @@
 #define RTG_CAT(a, b) RTG_CAT2(a, b)
 
 namespace rtg {
-TraceFn RTG_CAT(trace_fn_s, RTG_S)(bool lds, int variant) { return trace_fn<RTG_S>(lds, variant); }
+TraceFn RTG_CAT(trace_fn_s, RTG_S)(bool lds, int variant, bool bvh) {
+  return trace_fn<RTG_S>(lds, variant, bvh);
+}
 }  // namespace rtg

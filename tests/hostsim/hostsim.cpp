@@ -28,6 +28,27 @@ struct HostScene {
   const float* lights;
   unsigned n, m, n4;
   bool all(bool b) const { return b; }
+  bool any(bool b) const { return b; }
+  const float* bvhNodes = nullptr;
+  const float* bvhAux = nullptr;
+  const int* bvhChild = nullptr;
+  bool has_bvh() const { return bvhNodes != nullptr; }
+  int* bvh_stack() const { return nullptr; }
+  void bvh_node(unsigned nd, rtg::V3* c, float* w, int* ch) const {
+    for (int k = 0; k < 4; ++k) {
+      const float* g = bvhNodes + 16 * nd + 4 * k;
+      c[k] = rtg::v3(g[0], g[1], g[2]);
+      w[k] = g[3];
+      ch[k] = bvhChild[4 * nd + k];
+    }
+  }
+  void bvh_aux(unsigned nd, float* rp, float* cr) const {
+    for (int k = 0; k < 4; ++k) {
+      rp[k] = bvhAux[8 * nd + 2 * k];
+      cr[k] = bvhAux[8 * nd + 2 * k + 1];
+    }
+  }
+  float first_lane(float v) const { return v; }
   rtg::V3 sphere(unsigned i, float& r2) const {
     const float* g = geom + 4 * i;
     r2 = g[3];
@@ -86,6 +107,7 @@ struct HostScene {
 };
 
 int g_variant = 0;
+bool g_useBvh = true;
 
 template <int S>
 void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, float* out) {
@@ -143,6 +165,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 }  // namespace
 
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
+extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
 // the renders since the last reset (diagnostic; single-lane semantics, so the
 // wave unions of the GPU are per-sample masks here).
@@ -163,6 +186,11 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   if (rtg::make_camera(W, H, zoom, aa, &cam)) return -1;
   HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, m, ps.n4};
   sc.smask = ps.smask.empty() ? nullptr : ps.smask.data();
+  if (!ps.bvhChild.empty() && g_useBvh) {
+    sc.bvhNodes = ps.bvhNodes.data();
+    sc.bvhAux = ps.bvhAux.data();
+    sc.bvhChild = ps.bvhChild.data();
+  }
   for (unsigned k = 0; k < nrows; ++k) {
     float* o = out + (size_t)k * W * 3;
     switch (S) {
@@ -480,5 +508,116 @@ extern "C" long hostsim_contain_mask_check(long scenes, unsigned n, long points,
     }
   }
   if (tested) *tested = cnt;
+  return bad;
+}
+
+// BVH bounds against the reference's own root test (raytracer.h:81-141), on
+// adversarial ray/sphere pairs (near-tangent lines, far spheres, origins on
+// the surface, unnormalised directions, scales 1e-3..1e3):
+//  * bound screen (pass1_bound with K_B): for a node centre C at a random
+//    offset from the sphere and R = |c - C| + r (the tightest bound the
+//    builder makes), every accepted sphere passes;  -> *bad_screen
+//  * root distance (beyond): an accepted root t never lies nearer than
+//    |p| - r - 2^-8 (|p| + r) along the ray, so beyond() with reach just
+//    below t |d| never prunes it.  -> return value
+// *accepted counts accepted pairs.
+extern "C" long hostsim_bvh_bound_check(long trials, unsigned long long seed, long* accepted,
+                                        long* bad_screen) {
+  unsigned long long st = seed * 0x9E3779B97F4A7C15ull + 5;
+  auto u01 = [&]() {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  };
+  long bad = 0, badS = 0, acc = 0;
+  for (long t = 0; t < trials; ++t) {
+    const double scale = pow(10.0, -3.0 + 6.0 * u01());
+    rtg::V3 c = rtg::v3((float)((u01() - 0.5) * 20 * scale), (float)((u01() - 0.5) * 20 * scale),
+                        (float)((u01() - 0.5) * 20 * scale));
+    double dx = u01() - 0.5, dy = u01() - 0.5, dz = u01() - 0.5;
+    const double dl = sqrt(dx * dx + dy * dy + dz * dz);
+    const double dscale = (t % 3 == 0) ? 1.0 / dl : (0.1 + 3.0 * u01());
+    rtg::V3 d = rtg::v3((float)(dx * dscale), (float)(dy * dscale), (float)(dz * dscale));
+    rtg::V3 o;
+    float r;
+    const int mode = (int)(t % 4);
+    const double far = (t % 5 == 0) ? pow(10.0, 1.0 + 2.0 * u01()) : 1.0;  // far, small spheres
+    if (mode == 3) {  // origin on the sphere surface, random direction
+      r = (float)(scale * (0.1 + u01()));
+      double ux = u01() - 0.5, uy = u01() - 0.5, uz = u01() - 0.5;
+      const double ul = sqrt(ux * ux + uy * uy + uz * uz);
+      o = rtg::v3((float)(c.x + r * ux / ul), (float)(c.y + r * uy / ul), (float)(c.z + r * uz / ul));
+    } else {  // radius = distance(centre, line) * (1 +- tiny), or a far sphere
+              // the line misses by up to 3e-3 |p| (accepted only by rounding)
+      o = rtg::v3((float)(c.x + (u01() - 0.5) * 20 * scale * far),
+                  (float)(c.y + (u01() - 0.5) * 20 * scale * far),
+                  (float)(c.z + (u01() - 0.5) * 20 * scale * far));
+      const double px = (double)o.x - c.x, py = (double)o.y - c.y, pz = (double)o.z - c.z;
+      const double dd = (double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z;
+      const double pd = px * d.x + py * d.y + pz * d.z;
+      const double dist2 = px * px + py * py + pz * pz - pd * pd / dd;
+      const double dist = sqrt(fmax(dist2, 0.0));
+      if (t % 2 == 0 && far > 1.0) {
+        const double pl = sqrt(px * px + py * py + pz * pz);
+        r = (float)(dist - 3e-3 * pl * u01() * u01());
+        if (!(r > 0.f)) r = (float)(dist * 0.5);
+      } else {
+        const double rel = pow(10.0, -7.0 + 4.0 * u01()) * (u01() < 0.5 ? -1.0 : 1.0);
+        r = (float)(dist * (1.0 + rel));
+      }
+    }
+    if (t % 4 == 1) {  // tiny far sphere, line aimed just outside it: the
+                       // reference accepts misses of up to ~7e-4 |p| here
+      double ux = u01() - 0.5, uy = u01() - 0.5, uz = u01() - 0.5;
+      const double ul = sqrt(ux * ux + uy * uy + uz * uz);
+      ux /= ul; uy /= ul; uz /= ul;
+      const double L = scale * pow(10.0, 1.0 + 2.0 * u01());
+      o = rtg::v3((float)(c.x + L * ux), (float)(c.y + L * uy), (float)(c.z + L * uz));
+      const double rr = L * pow(10.0, -7.0 + 4.0 * u01());
+      const double miss = rr + L * 2e-3 * pow(u01(), 3);
+      double vx = u01() - 0.5, vy = u01() - 0.5, vz = u01() - 0.5;
+      const double vd = vx * ux + vy * uy + vz * uz;
+      vx -= vd * ux; vy -= vd * uy; vz -= vd * uz;
+      const double vl = sqrt(vx * vx + vy * vy + vz * vz) + 1e-300;
+      const double ds = 0.1 + 3 * u01();
+      d = rtg::v3((float)((c.x + miss * vx / vl - o.x) * ds / L),
+                  (float)((c.y + miss * vy / vl - o.y) * ds / L),
+                  (float)((c.z + miss * vz / vl - o.z) * ds / L));
+      r = (float)rr;
+    }
+    const float r2 = r * r;
+    const rtg::RayQ q = rtg::make_query(o, d);
+    bool res;
+    const float tr = rtg::ray_sphere(q, c, r2, res);
+    if (!res) continue;
+    ++acc;
+    // bound screen: node centre offset from c by up to 3 r (tightest R),
+    // mostly straight away from the line (the line's distance to C is then
+    // its distance to c plus the offset: the worst case)
+    double ox = u01() - 0.5, oy = u01() - 0.5, oz = u01() - 0.5;
+    if (t % 8 != 0) {
+      const double px = (double)o.x - c.x, py = (double)o.y - c.y, pz = (double)o.z - c.z;
+      const double dd = (double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z;
+      const double s = -(px * d.x + py * d.y + pz * d.z) / dd;  // closest point o + s d
+      ox = -(px + s * d.x); oy = -(py + s * d.y); oz = -(pz + s * d.z);  // c - X
+    }
+    const double ol = sqrt(ox * ox + oy * oy + oz * oz) + 1e-300;
+    const double off = (t % 4 == 1) ? sqrt((double)rtg::vdot(rtg::vsub(o, c), rtg::vsub(o, c))) *
+                                          pow(10.0, -3.0 + 3.0 * u01())
+                                    : 3.0 * fabs((double)r) * u01();
+    const rtg::V3 C = rtg::v3((float)(c.x + off * ox / ol), (float)(c.y + off * oy / ol),
+                              (float)(c.z + off * oz / ol));
+    const double cx = (double)c.x - C.x, cy = (double)c.y - C.y, cz = (double)c.z - C.z;
+    const double R = sqrt(cx * cx + cy * cy + cz * cz) + fabs((double)r);
+    const float w = rtg::bound_r2(R * (1.0 + 0x1p-20));
+    if (rtg::pass1_bound(q, C, w) < 0.f) ++badS;
+    // root distance: reach = 0.999999 t |d| must not prune the sphere itself
+    const float rp = rtg::round_up_f(fabs((double)r) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
+    const rtg::V3 p = rtg::vsub(o, c);
+    const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
+    const double tl = (double)tr * sqrt((double)q.den * 0.5) * (1.0 - 1e-6);
+    if (rtg::beyond(p2, rp, (float)tl)) ++bad;
+  }
+  if (accepted) *accepted = acc;
+  if (bad_screen) *bad_screen = badS;
   return bad;
 }

@@ -341,3 +341,41 @@ def test_overlap_masks_bound_containment(hostsim):
             ctypes.byref(tested))
     assert bad == 0, bad
     assert tested.value > 200_000, tested.value
+
+
+def test_bvh_bounds_are_conservative(hostsim):
+    """BVH node screens (pass1_bound, slack K_B = 2^-7) keep every sphere the
+    reference's root test accepts, and the distance prune (beyond) never drops
+    an accepted root, over 3M adversarial near-tangent / far / on-surface
+    ray-sphere pairs at scales 1e-3..1e3 (rtg_trace.h closest_bvh).  The
+    tiny-far-sphere cases (lines the reference accepts although they miss by
+    up to ~7e-4 |p|) need K_B >= ~2^-11.2: at 2^-12 this test fails."""
+    f = hostsim.hostsim_bvh_bound_check
+    f.restype = ctypes.c_long
+    acc, bad_screen = ctypes.c_long(0), ctypes.c_long(0)
+    bad = f(ctypes.c_long(3_000_000), ctypes.c_ulonglong(2026), ctypes.byref(acc),
+            ctypes.byref(bad_screen))
+    assert bad == 0 and bad_screen.value == 0, (bad, bad_screen.value)
+    assert acc.value > 500_000, acc.value
+
+
+def test_kernel_traversal_bvh_random_scenes(hostsim, oracle):
+    """Scenes above 64 spheres take the BVH queries (closest, shadow,
+    container); random scenes of 65..400 spheres, small and large radii,
+    overlapping clusters, bit-exact against the oracle."""
+    rng = np.random.default_rng(65)
+    hostsim.hostsim_set_variant(0)
+    for trial in range(12):
+        S = int(rng.integers(1, 9))
+        n, m = int(rng.integers(65, 400)), int(rng.integers(0, 5))
+        W, H = int(rng.integers(1, 24)), int(rng.integers(1, 18))
+        aa = float(rng.choice([1.0, 2.0, 3.0]))
+        zoom = float(rng.choice([-4.0, -2.0, 3.0]))
+        sph, lg = random_scene(rng, n, m)
+        if trial % 3 == 0:  # dense overlapping clusters
+            sph["pos"] *= 0.3
+        if zoom > 0:
+            sph["pos"][:, 2] *= -1.0
+        want = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
+        got = _hostsim_render(hostsim, sph, lg, W, H, S, aa=aa, zoom=zoom)
+        assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
