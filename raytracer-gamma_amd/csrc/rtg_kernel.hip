@@ -116,6 +116,7 @@ struct rtg_context {
   float* mats = nullptr;
   float* lights = nullptr;
   unsigned* smask = nullptr;  // shadow masks (null when the scene has none)
+  unsigned* cone = nullptr;   // secondary-ray cone masks (null when none)
   float* bvhNodes = nullptr;  // BVH (null when the scene has none)
   float* bvhAux = nullptr;
   int* bvhChild = nullptr;
@@ -136,6 +137,8 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->mats);
   (void)hipFree(c->lights);
   (void)hipFree(c->smask);
+  (void)hipFree(c->cone);
+  c->cone = nullptr;
   (void)hipFree(c->bvhNodes);
   (void)hipFree(c->bvhAux);
   (void)hipFree(c->bvhChild);
@@ -333,6 +336,15 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->smask, ps.smask.data(), ps.smask.size() * sizeof(unsigned),
                       hipMemcpyHostToDevice));
   }
+  if (!ps.cone.empty()) {
+    if (hipMalloc(&ctx->cone, ps.cone.size() * sizeof(unsigned)) != hipSuccess) {
+      free_scene(ctx);
+      rtg_set_error("hipMalloc failed for cone masks");
+      return RTG_ERR_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(ctx->cone, ps.cone.data(), ps.cone.size() * sizeof(unsigned),
+                      hipMemcpyHostToDevice));
+  }
   if (!ps.bvhChild.empty()) {
     if (hipMalloc(&ctx->bvhNodes, ps.bvhNodes.size() * sizeof(float)) != hipSuccess ||
         hipMalloc(&ctx->bvhAux, ps.bvhAux.size() * sizeof(float)) != hipSuccess ||
@@ -383,8 +395,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   const bool sampleKernel = vi->kind == kVariantSample;
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
-  if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 50 ||
-      variant == 110)
+  if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 20 ||
+      variant == 50 || variant == 110)
     ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr);
   if (!fn) {
@@ -412,6 +424,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.mats = ctx->mats;
   a.lights = ctx->lights;
   a.smask = ctx->smask;
+  a.cone = ctx->cone;
   a.bvhNodes = ctx->bvhNodes;
   a.bvhAux = ctx->bvhAux;
   a.bvhChild = ctx->bvhChild;

@@ -43,6 +43,9 @@ struct PackedScene {
   // masks, each {lo, hi} words, for 1 <= n <= 64 and a finite scene; empty
   // otherwise (every sphere is then tested).
   std::vector<unsigned> smask;
+  // Secondary-ray cone masks (cone_masks): n x kConeTiers x kConeCells x {lo, hi}, with
+  // the sphere masks; empty otherwise.
+  std::vector<unsigned> cone;
   // BVH of scenes above kMaskMaxSpheres spheres (build_bvh): per node 4
   // slots {x, y, z, screen radius^2} (bound_r2 for a child node, screen_r2
   // for a sphere), 4 children (> 0 node, < 0 ~sphere index, 0 empty) and 4
@@ -186,6 +189,91 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
       const double rj = fabs((double)sj.radius) + 1e-6;
       const double mu = 0x1p-8 * (d + g + rj);
       if (!(d > (reach + rj + mu) * (1.0 + 1e-9))) w[j >> 5] |= 1u << (j & 31);
+    }
+  }
+}
+
+// Secondary-ray cone masks.  A secondary ray of sphere h starts in the origin
+// ball B''_h = ball(c_h, rho_h), rho_h = g_h + 0.0101 + 2^-20 (|c_h| + g_h):
+// refraction children start at the hit point P (|P - c_h| <= g_h, the guard
+// test) and reflection children at P + 0.01f rd with |rd| = 1 (vnorm)
+// (raytracer.h:830-836).  Sphere i can take an accepted root (t > 1e-5) only
+// if the ray points into the cone of directions from B''_h to ball(c_i, r'_i),
+// r'_i = |r_i| + mu_i, mu_i = 2^-8 (D + rho_h + |r_i|) (D = |c_i - c_h|; the
+// shadow masks' margin for the reference's rounding): its axis is
+// u = (c_i - c_h) / D and its half-angle is at most
+//   alpha = asin(r'_i / (D - rho_h)) + asin(rho_h / D)
+// (every sphere when D <= rho_h + r'_i, and sphere h itself).  The kernel
+// uses the masks of (h, tier, cell(U)) when every active lane's direction lies
+// within the tier's half-angle kConeHalf[tier] of the first lane's U; U lies
+// in its cube-map cell, whose directions are within beta (the largest angle
+// from the cell's centre direction to a corner) of that centre.  So sphere i
+// is in mask (h, tier, cell) when angle(centre, u) <= alpha + kConeHalf[tier]
+// + beta + 1e-3 (the 1e-3 rad covers the float direction estimates and cell
+// borders).  tests/test_oracle.py::test_cone_masks_are_conservative.
+inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsigned>* out) {
+  out->assign((size_t)n * kConeTiers * kConeCells * 2, 0u);
+  const double kPi = 3.14159265358979323846;
+  // cell centres and radii
+  std::vector<double> cc((size_t)kConeCells * 3), cb(kConeCells);
+  for (int face = 0; face < 6; ++face)
+    for (int ia = 0; ia < kConeGrid; ++ia)
+      for (int ib = 0; ib < kConeGrid; ++ib) {
+        const int cell = (face * kConeGrid + ia) * kConeGrid + ib;
+        const int major = face / 2;
+        const double sg = (face % 2 == 0) ? 1.0 : -1.0;
+        const int ax = major == 0 ? 1 : 0, bx = major == 2 ? 1 : 2;
+        auto dirv = [&](double a, double b, double* v) {
+          v[0] = v[1] = v[2] = 0.0;
+          v[major] = sg;
+          v[ax] = a;
+          v[bx] = b;
+          const double l = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+          for (int k = 0; k < 3; ++k) v[k] /= l;
+        };
+        const double a0 = -1.0 + 2.0 * ia / kConeGrid, a1 = a0 + 2.0 / kConeGrid;
+        const double b0 = -1.0 + 2.0 * ib / kConeGrid, b1 = b0 + 2.0 / kConeGrid;
+        double c[3];
+        dirv(0.5 * (a0 + a1), 0.5 * (b0 + b1), c);
+        double beta = 0.0;
+        const double corners[4][2] = {{a0, b0}, {a0, b1}, {a1, b0}, {a1, b1}};
+        for (const auto& co : corners) {
+          double v[3];
+          dirv(co[0], co[1], v);
+          const double dt = c[0] * v[0] + c[1] * v[1] + c[2] * v[2];
+          beta = fmax(beta, acos(fmin(1.0, fmax(-1.0, dt))));
+        }
+        for (int k = 0; k < 3; ++k) cc[(size_t)cell * 3 + k] = c[k];
+        cb[cell] = beta;
+      }
+  for (unsigned h = 0; h < n; ++h) {
+    const rtg_sphere& sh = spheres[h];
+    const double ch = fabs((double)sh.pos.x) + fabs((double)sh.pos.y) + fabs((double)sh.pos.z);
+    const double g = guard_radius(sh);
+    const double rho = g + 0.0101 + 0x1p-20 * (ch + g);
+    for (unsigned i = 0; i < n; ++i) {
+      const rtg_sphere& si = spheres[i];
+      const double ux = (double)si.pos.x - sh.pos.x, uy = (double)si.pos.y - sh.pos.y,
+                   uz = (double)si.pos.z - sh.pos.z;
+      const double D = sqrt(ux * ux + uy * uy + uz * uz);
+      const double ri = fabs((double)si.radius);
+      const double rr = ri + 0x1p-8 * (D + rho + ri);
+      bool all = (i == h) || !(D > (rho + rr) * (1.0 + 1e-9));
+      double alpha = 0.0;
+      if (!all) alpha = asin(fmin(1.0, rr / (D - rho))) + asin(fmin(1.0, rho / D));
+      for (int tier = 0; tier < kConeTiers; ++tier)
+        for (int cell = 0; cell < kConeCells; ++cell) {
+          bool keep = all || alpha + kConeHalf[tier] + 1e-3 >= kPi;
+          if (!keep) {
+            const double* c = &cc[(size_t)cell * 3];
+            const double dt = (c[0] * ux + c[1] * uy + c[2] * uz) / D;
+            const double ang = acos(fmin(1.0, fmax(-1.0, dt)));
+            keep = !(ang > alpha + kConeHalf[tier] + cb[cell] + 1e-3);
+          }
+          if (keep)
+            (*out)[(((size_t)h * kConeTiers + tier) * kConeCells + cell) * 2 + (i >> 5)] |=
+                1u << (i & 31);
+        }
     }
   }
 }
@@ -361,6 +449,8 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   }
   ps->mats[(size_t)n * 8 + 7] = 1.00f;
   shadow_masks(spheres, n, lights, m, &ps->smask);
+  if (!ps->smask.empty()) cone_masks(spheres, n, &ps->cone);
+  else ps->cone.clear();
   build_bvh(spheres, n, ps);
   for (unsigned l = 0; l < m; ++l) {
     float* p = &ps->lights[(size_t)l * 6];

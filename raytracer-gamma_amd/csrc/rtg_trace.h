@@ -129,6 +129,15 @@ RTG_HD float rcp_rn(float b) {
   }
   return y;
 }
+// Approximate reciprocal square root (v_rsq_f32, ~1 ulp) for conservative
+// culls only (primary_sphere_possible, the cone cull); never for results.
+RTG_HD float cull_rsq(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rsqf(x);
+#else
+  return 1.0f / sqrtf(x);
+#endif
+}
 RTG_HD float rtg_sqrtf(float x) { return sqrt_rn(x); }
 // vec.h:41: l = 1.f / sqrt(dot); v *= l.
 RTG_HD V3 vnorm(V3 v) { float l = rcp_rn(rtg_sqrtf(vdot(v, v))); return vsmul(l, v); }
@@ -150,7 +159,7 @@ struct Mat { V3 matte, gloss; float opacity, refr; };
 enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, kCntEnterOK,
              kCntFullQ, kCntFullCand, kCntShadowQ, kCntShadowSel, kCntShadowCand,
              kCntContainMasked, kCntContainSel, kCntContainFull, kCntRefraction, kCntReflPush,
-             kCntBvhNodeTests, kCntBvhSphereTests, kCntSlots };
+             kCntBvhNodeTests, kCntBvhSphereTests, kCntConeQ, kCntConeSel, kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
@@ -160,7 +169,8 @@ enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTo
 // the pre-computed reflection ray is only read when that child is traced.
 struct FrameC {
   float cx, cy, cz;
-  unsigned meta;  // rm << 2 | flags (bit0: stage 2, bit1: reflection child significant)
+  unsigned meta;  // rm << 9 | (1 + origin sphere) << 2 | flags (bit0: stage 2,
+                  // bit1: reflection child significant)
 };
 struct FrameR { V3 ro, rd, rI; };
 
@@ -345,6 +355,39 @@ RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel) {
   return found;
 }
 
+// Direction cells of the secondary-ray cull (cone_masks, rtg_scene_pack.h):
+// a cube map of kConeGrid x kConeGrid cells per face.  A wave whose active
+// lanes all trace rays from sphere origin balls (h_lane) and whose directions
+// all lie within a bundle half-angle of the first lane's direction U tests
+// only the union over its lanes' h of mask (h, tier, cell(U)); two tiers of
+// bundle half-angle, the tighter one used when it holds.
+constexpr int kConeGrid = 8;
+constexpr int kConeCells = 6 * kConeGrid * kConeGrid;
+constexpr int kConeTiers = 2;
+constexpr double kConeHalf[kConeTiers] = {0.20943951023931953,   // 12 degrees
+                                          0.61086523819801535};  // 35 degrees
+constexpr float kConeCos[kConeTiers] = {0.97814760073380569f,   // cos, rounded up
+                                        0.81915204428899179f};
+
+// Cube-map cell of direction U (any length): the face of the major axis and
+// a kConeGrid x kConeGrid grid over the other two coordinates / |major|.  A
+// direction near a cell border may land in either cell; the masks' 1e-3 rad
+// margin covers that.
+RTG_HD int cone_cell(V3 U) {
+  const float ax = fabsf(U.x), ay = fabsf(U.y), az = fabsf(U.z);
+  int face;
+  float m, a, b;
+  if (ax >= ay && ax >= az) { face = U.x > 0.f ? 0 : 1; m = ax; a = U.y; b = U.z; }
+  else if (ay >= az) { face = U.y > 0.f ? 2 : 3; m = ay; a = U.x; b = U.z; }
+  else { face = U.z > 0.f ? 4 : 5; m = az; a = U.x; b = U.y; }
+  const float im = 1.f / m;
+  int ia = (int)((a * im + 1.f) * (0.5f * kConeGrid));
+  int ib = (int)((b * im + 1.f) * (0.5f * kConeGrid));
+  ia = ia < 0 ? 0 : (ia > kConeGrid - 1 ? kConeGrid - 1 : ia);
+  ib = ib < 0 ? 0 : (ib > kConeGrid - 1 ? kConeGrid - 1 : ib);
+  return (face * kConeGrid + ia) * kConeGrid + ib;
+}
+
 // Query strategies (defined below): see query_closest / query_blocked.
 template <int Q, class Scene>
 RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t);
@@ -505,6 +548,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
   int rm = (int)sc.n;                   // background material
   int enterH = -1;  // Q == 4: the sphere this ray entered (refraction child), or -1
+  int originH = -1;  // Q == 4: the sphere whose origin ball holds this ray's origin, or -1
   for (;;) {
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
@@ -522,11 +566,28 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       sc.count(kCntEnterQ, 1);
       sc.count(kCntEnterOK, ok ? 1 : 0);
       if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
+    } else if (Q == 4 && sc.has_cone() && sc.all(originH >= 0)) {
+      // secondary rays from sphere origin balls in a narrow bundle: only the
+      // spheres of their cone masks for the bundle's cell
+      const V3 dh = vsmul(cull_rsq(vdot(d, d)), d);  // about unit length
+      const V3 U = sc.first_lane(dh);
+      const float cu = vdot(dh, U);
+      const int tier = sc.all(cu >= kConeCos[0]) ? 0 : sc.all(cu >= kConeCos[1]) ? 1 : -1;
+      if (tier >= 0) {
+        const uint64_t cm = sc.cone_union(originH, (unsigned)tier, (unsigned)cone_cell(U));
+        sc.count(kCntConeQ, 1);
+        sc.count(kCntConeSel, __builtin_popcountll(cm));
+        hit = closest_sel(sc, make_query(o, d), cm, t);
+      } else {
+        sc.count(kCntFullQ, 1);
+        hit = query_closest<2>(sc, o, d, t);
+      }
     } else {
       sc.count(kCntFullQ, 1);
       hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
     }
     enterH = -1;
+    originH = -1;
     sc.probe_end(kProbeClosest);
     sc.probe_begin(kProbeShade);
     if (hit < 0) {
@@ -575,7 +636,10 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           const int lv = sp < NF ? sp : NF - 1;
           FrameC& f = fc(lv);
           f.cx = colour.x; f.cy = colour.y; f.cz = colour.z;
-          f.meta = ((unsigned)rm << 2) | (sigR ? 2u : 0u);
+          // bits 2..8: 1 + the sphere whose origin ball holds the
+          // reflection ray's origin P + 0.01 rd (cone cull, n <= 64), or 0
+          f.meta = ((unsigned)rm << 9) |
+                   ((unsigned)(sc.has_cone() && guardOK ? hit + 1 : 0) << 2) | (sigR ? 2u : 0u);
           if (sigR) {
             sc.count(kCntReflPush, 1);
             // calculateReflection, raytracer.h:817-842
@@ -590,6 +654,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           // refraction child: calculateRefraction's refracted ray (:805-809);
           // hit from outside (cosA1 < 0): the child starts in sphere `hit`
           if (Q == 4 && vdot(d, N) < 0.f) enterH = hit;
+          if (Q == 4 && guardOK && sc.has_cone()) originH = hit;  // the child starts at P
           I = vsmul((1.f - R), vsmul(tr, I));
           o = P;
           d = cdir;
@@ -619,7 +684,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       if ((f.meta & 3u) == 2u) {                              // stage 1, reflection
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
-        o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 2);
+        o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 9);
+        originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
         descend = true;
         break;
@@ -1129,6 +1195,35 @@ RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, boo
   return best;
 }
 
+// Closest hit of any ray over a wave-uniform subset `sel` of spheres 0..63
+// that holds every sphere the ray can hit (cone_masks): pass 1 screens the
+// spheres of `sel` (one scalar load each), pass 2 tests the lane's candidates
+// in index order, so the answer is closest_hit_mask's.
+template <class Scene>
+RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
+  uint64_t cand = 0;
+  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+    const unsigned i = (unsigned)__builtin_ctzll(m);
+    float rs;
+    const V3 c = sc.sphere_screen(i, rs);
+    cand |= (pass1_rad(q, c, rs) < 0.f) ? 0ull : (1ull << i);
+  }
+  float minT = 1000.f;
+  int best = -1;
+  while (cand) {
+    const unsigned i = (unsigned)__builtin_ctzll(cand);
+    cand &= cand - 1;
+    sc.count(kCntFullCand, 1);
+    float r2;
+    const V3 c = sc.sphere_lane(i, r2);
+    bool res;
+    const float t = ray_sphere(q, c, r2, res);
+    if (res && t < minT) { minT = t; best = (int)i; }
+  }
+  tOut = minT;
+  return best;
+}
+
 // Closest hit restricted to a wave-uniform subset `sel` of spheres 0..63
 // (bit i = sphere i may be hit; see primary_sphere_mask).  Spheres outside
 // `sel` cannot produce a valid root, so the result equals closest_hit_mask's.
@@ -1178,13 +1273,6 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
 // roots used here (about 1 ulp) and of the reference's own root test.
 // Bundles wider than 60 degrees, and spheres at or around the origin, are
 // never culled.
-RTG_HD float cull_rsq(float x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_rsqf(x);
-#else
-  return 1.0f / sqrtf(x);
-#endif
-}
 
 RTG_HD bool primary_sphere_possible(V3 c, float r, float x0, float x1, float y0, float y1,
                                     float zoom) {

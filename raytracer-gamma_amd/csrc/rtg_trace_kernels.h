@@ -81,6 +81,7 @@ struct DevScene {
   const float4* lgeom;  // LDS copy of geom (or the global array when it does not fit)
   cfloat_p lights;
   cuint_p smask;  // m x n x {lo, hi} shadow masks, or null
+  cuint_p cone;   // n x kConeCells x {lo, hi} secondary-ray cone masks, or null
   cfloat_p bvhNodes;  // BVH (build_bvh, rtg_scene_pack.h) or null
   int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
   cfloat_p bvhAux;
@@ -141,9 +142,28 @@ struct DevScene {
       cr[k] = g[2 * k + 1];
     }
   }
-  // One lane's value for wave-uniform decisions (traversal order only).
+  // One lane's value for wave-uniform decisions (traversal order, cone cull).
   __device__ __forceinline__ float first_lane(float v) const {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+  }
+  __device__ __forceinline__ V3 first_lane(V3 v) const {
+    return v3(first_lane(v.x), first_lane(v.y), first_lane(v.z));
+  }
+  // Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): n <= 64.
+  __device__ __forceinline__ bool has_cone() const { return cone != nullptr; }
+  // Union over the active lanes' origin spheres h (all >= 0) of cone mask
+  // (h, tier, cell): one scalar load per distinct h.
+  __device__ __forceinline__ uint64_t cone_union(int h, unsigned tier, unsigned cell) const {
+    uint64_t todo = __ballot(1);
+    uint64_t u = 0;
+    while (todo) {
+      const int src = __builtin_ctzll(todo);
+      const int h0 = __builtin_amdgcn_readlane(h, src);
+      const cuint_p w = cone + 2u * (((unsigned)h0 * kConeTiers + tier) * kConeCells + cell);
+      u |= (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      todo &= ~__ballot(h == h0);
+    }
+    return u;
   }
   // Shadow and overlap masks (rtg_scene_pack.h shadow_masks): n <= 64.
   __device__ __forceinline__ bool has_smask() const { return smask != nullptr; }
@@ -210,6 +230,7 @@ struct KernelArgs {
   const float* mats;
   const float* lights;
   const unsigned* smask;  // shadow masks (PackedScene::smask) or null
+  const unsigned* cone;   // cone masks (PackedScene::cone) or null
   const float* bvhNodes;  // BVH (PackedScene::bvh*) or null
   const float* bvhAux;
   const int* bvhChild;
@@ -263,6 +284,7 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.crad2 = (cfloat_p)a.crad2;
   sc.lights = (cfloat_p)a.lights;
   sc.smask = (cuint_p)a.smask;
+  sc.cone = (cuint_p)a.cone;
   sc.bvhNodes = (cfloat_p)a.bvhNodes;
   // BVH scenes: 64 stack entries per wave after the frames and scene tables
   // (the launcher adds them to the LDS size).
@@ -519,6 +541,7 @@ void trace_samples_kernel(const KernelArgs a) {
   DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh> sc;
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
+  if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screen every sphere)
   trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
@@ -545,6 +568,7 @@ void trace_samples_kernel(const KernelArgs a) {
 //   15 as 0 with shadow rays screening every sphere (no shadow masks)
 //   18 as 0 built for 8 waves per SIMD (<= 64 VGPRs)
 //   19 as 0 with shuffle reductions for the cull bounds and the pixel sum
+//   20 as 0 without the secondary-ray cone cull (cone_masks)
 //   50 / 59: 0 / 9 with the OpenCL kernel's semantics (RTG_SEMANTICS_OPENCL;
 //     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
@@ -570,6 +594,7 @@ constexpr VariantInfo kVariants[] = {
     {6, kVariantTile, false},    {8, kVariantTile, false},    {9, kVariantTile, false},
     {14, kVariantSample, false}, {15, kVariantSample, false}, {16, kVariantSample, false},
     {17, kVariantSample, false}, {18, kVariantSample, false}, {19, kVariantSample, false},
+    {20, kVariantSample, false},
     {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
     {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
 };
@@ -583,7 +608,7 @@ template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 50 || V == 110)
+  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 20 || V == 50 || V == 110)
     return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -613,6 +638,7 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh) {
     case 110: return trace_fn_v<S, 110>(lds);
     case 18: return trace_fn_v<S, 18>(lds);
     case 19: return trace_fn_v<S, 19>(lds);
+    case 20: return trace_fn_v<S, 20>(lds);
     case 50: return trace_fn_v<S, 50>(lds);
     case 59: return trace_fn_v<S, 59>(lds);
     case 104: return trace_fn_v<S, 104>(lds);

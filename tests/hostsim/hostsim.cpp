@@ -33,6 +33,14 @@ struct HostScene {
   const float* bvhAux = nullptr;
   const int* bvhChild = nullptr;
   bool has_bvh() const { return bvhNodes != nullptr; }
+  const unsigned* cone = nullptr;
+  bool has_cone() const { return cone != nullptr; }
+  rtg::V3 first_lane(rtg::V3 v) const { return v; }
+  uint64_t cone_union(int h, unsigned tier, unsigned cell) const {
+    const unsigned* w =
+        cone + 2u * (((unsigned)h * rtg::kConeTiers + tier) * rtg::kConeCells + cell);
+    return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  }
   int* bvh_stack() const { return nullptr; }
   void bvh_node(unsigned nd, rtg::V3* c, float* w, int* ch) const {
     for (int k = 0; k < 4; ++k) {
@@ -186,6 +194,7 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   if (rtg::make_camera(W, H, zoom, aa, &cam)) return -1;
   HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, m, ps.n4};
   sc.smask = ps.smask.empty() ? nullptr : ps.smask.data();
+  sc.cone = ps.cone.empty() ? nullptr : ps.cone.data();
   if (!ps.bvhChild.empty() && g_useBvh) {
     sc.bvhNodes = ps.bvhNodes.data();
     sc.bvhAux = ps.bvhAux.data();
@@ -619,5 +628,99 @@ extern "C" long hostsim_bvh_bound_check(long trials, unsigned long long seed, lo
   }
   if (accepted) *accepted = acc;
   if (bad_screen) *bad_screen = badS;
+  return bad;
+}
+
+// Cone masks (cone_masks, rtg_scene_pack.h) against the reference's own root
+// test: random scenes; for random (h, i), an origin in h's origin ball
+// (mostly on its boundary towards i), a direction d aimed at a point of
+// sphere i's silhouette (grazing, in or slightly out), and a bundle direction
+// U up to kConeHalf away from d; if i is not in mask (h, cone_cell(U)) the
+// reference must not accept a root of sphere i.  Returns the violations;
+// *tested counts the rays the reference accepts for sphere i.
+extern "C" long hostsim_cone_mask_check(long scenes, unsigned n, long rays,
+                                        unsigned long long seed, long* tested) {
+  unsigned long long st = seed * 0x9E3779B97F4A7C15ull + 3;
+  auto u01 = [&]() {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  };
+  auto unit = [&](double* v) {
+    double l;
+    do {
+      for (int k = 0; k < 3; ++k) v[k] = 2.0 * u01() - 1.0;
+      l = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    } while (l < 1e-3 || l > 1.0);
+    for (int k = 0; k < 3; ++k) v[k] /= l;
+  };
+  long bad = 0, cnt = 0;
+  std::vector<rtg_sphere> sph(n);
+  for (long sc = 0; sc < scenes; ++sc) {
+    const double scale = pow(10.0, -1.5 + 3.0 * u01());
+    for (unsigned i = 0; i < n; ++i) {
+      memset(&sph[i], 0, sizeof(rtg_sphere));
+      sph[i].pos.x = (float)((u01() - 0.5) * 24 * scale);
+      sph[i].pos.y = (float)((u01() - 0.5) * 16 * scale);
+      sph[i].pos.z = (float)((-6 - 34 * u01()) * scale);
+      sph[i].radius = (float)((0.2 + 3 * u01()) * scale);
+    }
+    std::vector<unsigned> masks;
+    rtg::cone_masks(sph.data(), n, &masks);
+    for (long r = 0; r < rays; ++r) {
+      const unsigned h = (unsigned)(u01() * n) % n, i = (unsigned)(u01() * n) % n;
+      if (i == h) continue;
+      const rtg_sphere& sh = sph[h];
+      const rtg_sphere& si = sph[i];
+      const double ch = fabs((double)sh.pos.x) + fabs((double)sh.pos.y) + fabs((double)sh.pos.z);
+      const double g = rtg::guard_radius(sh);
+      const double rho = g + 0.0101 + 0x1p-20 * (ch + g);
+      // origin: on the origin ball's boundary, biased towards i
+      double v[3];
+      unit(v);
+      const double ci[3] = {si.pos.x, si.pos.y, si.pos.z}, chv[3] = {sh.pos.x, sh.pos.y, sh.pos.z};
+      double w[3] = {ci[0] - chv[0], ci[1] - chv[1], ci[2] - chv[2]};
+      const double wl = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) + 1e-300;
+      const double bias = u01();
+      for (int k = 0; k < 3; ++k) v[k] = bias * w[k] / wl + (1.0 - bias) * v[k];
+      const double vl = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]) + 1e-300;
+      const double orad = rho * (r % 4 == 0 ? u01() : 1.0 - 1e-9);
+      double O[3];
+      for (int k = 0; k < 3; ++k) O[k] = chv[k] + orad * v[k] / vl;
+      // target on i's silhouette as seen from O, pushed out by up to 1e-3 r_i
+      double a[3] = {ci[0] - O[0], ci[1] - O[1], ci[2] - O[2]};
+      const double al = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]) + 1e-300;
+      double p[3];
+      unit(p);
+      const double pd = (p[0] * a[0] + p[1] * a[1] + p[2] * a[2]) / al;
+      for (int k = 0; k < 3; ++k) p[k] -= pd * a[k] / al;
+      const double pl = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]) + 1e-300;
+      const double off = fabs((double)si.radius) * (1.0 + 1e-3 * (u01() - 0.3));
+      double d[3];
+      for (int k = 0; k < 3; ++k) d[k] = ci[k] + off * p[k] / pl - O[k];
+      // bundle direction U: d rotated by up to kConeHalf
+      const double dl = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-300;
+      double q[3];
+      unit(q);
+      const double qd = (q[0] * d[0] + q[1] * d[1] + q[2] * d[2]) / dl;
+      for (int k = 0; k < 3; ++k) q[k] -= qd * d[k] / dl;
+      const double ql = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) + 1e-300;
+      const unsigned tier = (unsigned)(r & 1);
+      const double ang = rtg::kConeHalf[tier] * (r % 3 == 0 ? u01() : 1.0 - 1e-6);
+      double U[3];
+      for (int k = 0; k < 3; ++k) U[k] = cos(ang) * d[k] / dl + sin(ang) * q[k] / ql;
+      const int cell = rtg::cone_cell(rtg::v3((float)U[0], (float)U[1], (float)U[2]));
+      const unsigned* mw = &masks[(((size_t)h * rtg::kConeTiers + tier) * rtg::kConeCells + cell) * 2];
+      const double ds = 0.2 + 2.0 * u01();
+      const rtg::RayQ qr = rtg::make_query(
+          rtg::v3((float)O[0], (float)O[1], (float)O[2]),
+          rtg::v3((float)(d[0] / dl * ds), (float)(d[1] / dl * ds), (float)(d[2] / dl * ds)));
+      bool res;
+      rtg::ray_sphere(qr, rtg::v3(si.pos.x, si.pos.y, si.pos.z), si.radius * si.radius, res);
+      if (!res) continue;
+      ++cnt;
+      if (!(mw[i >> 5] & (1u << (i & 31)))) ++bad;
+    }
+  }
+  if (tested) *tested = cnt;
   return bad;
 }

@@ -379,3 +379,18 @@ def test_kernel_traversal_bvh_random_scenes(hostsim, oracle):
         want = oracle.render(sph, lg, W, H, S, aa=aa, zoom=zoom)
         got = _hostsim_render(hostsim, sph, lg, W, H, S, aa=aa, zoom=zoom)
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
+
+
+def test_cone_masks_are_conservative(hostsim):
+    """Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): a sphere left
+    out of mask (h, cell(U)) is never hit, by the reference's own root test,
+    by a ray from h's origin ball whose direction is within kConeHalf of U:
+    grazing rays aimed at that sphere's silhouette from the ball's boundary,
+    with U at the edge of the bundle, over random scenes at scales 0.03..30."""
+    f = hostsim.hostsim_cone_mask_check
+    f.restype = ctypes.c_long
+    tested = ctypes.c_long(0)
+    bad = f(ctypes.c_long(300), 16, ctypes.c_long(4000), ctypes.c_ulonglong(31),
+            ctypes.byref(tested))
+    assert bad == 0, bad
+    assert tested.value > 200_000, tested.value
