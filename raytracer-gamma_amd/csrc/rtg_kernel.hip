@@ -95,6 +95,72 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
     out[i] = ppm_byte(c[i], m);
 }
 
+// Trivial-group pass of the compacted launch: one LANE per pixel group (the
+// sample kernel's floor(64 / nAA^2) consecutive pixels).  The group's
+// primary-ray bundle is bounded from primary_bounds of each of its pixels
+// (the extremes of sample_dir's monotone float steps, as trace_group's cull)
+// and tested against every sphere with primary_sphere_possible.  A group no
+// sphere can be reached from is written directly: every sample misses
+// (closest_hit_sel over an empty set, raytracer.h:454-459), returns
+// I (x) bgMaterial.matte = (1,1,1) (x) 0 = +0 (raytracer.h:544, the
+// background matte is 0), and the pixel sum of +0 * inv is +0 in every
+// channel.  The other groups are appended to groupList (one atomic per wave)
+// for the trace kernel.  n <= 64 spheres.
+__global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
+                                                          unsigned* groupList,
+                                                          unsigned* groupCount) {
+  const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const unsigned nAA = (unsigned)a.cam.nAA;
+  const unsigned PPW = 64u / (nAA * nAA);
+  const size_t total = (size_t)a.W * a.rowsLocal;
+  bool possible = false;
+  size_t p0 = 0;
+  unsigned nv = 0;
+  if (g < nGroups) {
+    p0 = g * PPW;
+    nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);
+    unsigned col, lr;
+    divmod_u64(p0, a.W, lr, col);
+    float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
+    for (unsigned k = 0; k < nv; ++k) {
+      const unsigned gy = a.rowList ? a.rowList[lr]
+                                    : shard_global_row_fast(lr, a.rowBlock, a.shard, a.nShards);
+      float bx0, bx1, by0, by1;
+      primary_bounds(a.cam, col, gy, bx0, bx1, by0, by1);
+      x0 = fminf(x0, bx0);
+      x1 = fmaxf(x1, bx1);
+      y0 = fminf(y0, by0);
+      y1 = fmaxf(y1, by1);
+      if (++col == a.W) {
+        col = 0;
+        ++lr;
+      }
+    }
+    const RTG_CONST float* geom = (const RTG_CONST float*)a.geom;
+    for (unsigned i = 0; i < a.n; ++i) {  // wave-uniform: scalar sphere records
+      const RTG_CONST float* r = geom + 4 * i;
+      possible = possible ||
+                 primary_sphere_possible(v3(r[0], r[1], r[2]), sqrtf(r[3]), x0, x1, y0, y1,
+                                         a.cam.zoom);
+    }
+  }
+  if (g < nGroups && !possible) {
+    float* o = a.dst + p0 * 3;
+    for (unsigned k = 0; k < nv * 3; ++k) o[k] = 0.f;
+  }
+  const bool append = g < nGroups && possible;
+  const uint64_t m = __ballot(append);
+  if (m) {
+    const unsigned lane = threadIdx.x & 63u;
+    const int leader = __builtin_ctzll(m);
+    unsigned base = 0;
+    if ((int)lane == leader) base = atomicAdd(groupCount, (unsigned)__builtin_popcountll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (append) groupList[base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] = (unsigned)g;
+  }
+}
+
 static TraceFn pick_trace(int S, bool lds, int variant, bool bvh) {
   switch (S) {
 #define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant, bvh);
@@ -123,6 +189,11 @@ struct rtg_context {
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
+  unsigned* groupList = nullptr;  // compacted launch: listed pixel groups
+  unsigned* groupCount = nullptr;
+  size_t groupCap = 0;
+  int numCU = 256;
+  int persistPerCU = 0;  // > 0: fixed persistent waves per CU (RTG_PERSIST_PER_CU A/B knob)
   size_t timelineCap = 0, timelineCount = 0;
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
@@ -208,6 +279,14 @@ int rtg_context_create(int device, rtg_context** out) {
   HIP_TRY(hipSetDevice(device));
   rtg_context* c = new rtg_context();
   c->device = device;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      cus > 0)
+    c->numCU = cus;
+  if (const char* v = getenv("RTG_PERSIST_PER_CU")) {  // A/B knob (performance only)
+    const int k = atoi(v);
+    if (k >= 1 && k <= 4096) c->persistPerCU = k;
+  }
   if (const char* v = getenv("RTG_VARIANT")) {  // A/B knob
     char* end = nullptr;
     const long var = strtol(v, &end, 10);
@@ -237,6 +316,8 @@ int rtg_context_destroy(rtg_context* ctx) {
   (void)hipFree(ctx->maxScratch);
   (void)hipFree(ctx->diag);
   (void)hipFree(ctx->timeline);
+  (void)hipFree(ctx->groupList);
+  (void)hipFree(ctx->groupCount);
   delete ctx;
   return RTG_OK;
 }
@@ -396,7 +477,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
   if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 20 ||
-      variant == 50 || variant == 110)
+      variant == 21 || variant == 22 || variant == 50 || variant == 110)
     ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr);
   if (!fn) {
@@ -415,6 +496,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     rows = shard_row_count(height, rowBlock, shard, nShards);
   }
   if (rows == 0) return RTG_OK;
+  if ((double)width * rows >= 0x1p53) {  // divmod_u64's range (rtg_trace_kernels.h)
+    rtg_set_error("render: frame too large (%u x %u)", width, rows);
+    return RTG_ERR_INVALID;
+  }
   if (!dstDevice) {
     rtg_set_error("render: null destination");
     return RTG_ERR_INVALID;
@@ -440,6 +525,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.dst = reinterpret_cast<float*>(dstDevice);
   a.diag = nullptr;
   a.timeline = nullptr;
+  a.groupList = nullptr;
+  a.groupCount = nullptr;
+  a.nPersist = 0;
   if (variant >= 100) {
     if (!ctx->diag) {
       HIP_TRY(hipMalloc(&ctx->diag, 8 * sizeof(unsigned long long)));
@@ -451,7 +539,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
   if (sampleKernel) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
-    const size_t waves = ((size_t)width * rows + ppw - 1) / ppw;
+    const size_t groupsPerWave = variant == 21 ? 4 : 1;
+    const size_t groups = ((size_t)width * rows + ppw - 1) / ppw;
+    const size_t waves = (groups + groupsPerWave - 1) / groupsPerWave;
     const unsigned tpb = variant == 14 ? 256u : variant == 16 ? 128u : 64u;
     const size_t blocks = (waves + tpb / 64 - 1) / (tpb / 64);
     threads = tpb;
@@ -460,6 +550,35 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       return RTG_ERR_INVALID;
     }
     grid = dim3((unsigned)blocks, 1);
+    // Compacted launch (the default; variant 22 and the multi-wave-workgroup
+    // variants launch one wave per group instead): a cull pass writes the
+    // groups no primary ray can leave (+0) and lists the others; a grid of
+    // one-wave workgroups traces the listed groups round-robin.
+    const bool compact = tpb == 64 && variant != 21 && variant != 22;
+    if (compact && ctx->n <= 64 && groups <= 0xFFFFFFFFull) {
+      if (ctx->groupCap < groups) {
+        (void)hipFree(ctx->groupList);
+        ctx->groupList = nullptr;
+        ctx->groupCap = 0;
+        HIP_TRY(hipMalloc(&ctx->groupList, groups * sizeof(unsigned)));
+        ctx->groupCap = groups;
+      }
+      if (!ctx->groupCount) HIP_TRY(hipMalloc(&ctx->groupCount, sizeof(unsigned)));
+      HIP_TRY(hipMemsetAsync(ctx->groupCount, 0, sizeof(unsigned), (hipStream_t)stream));
+      hipLaunchKernelGGL(cull_groups_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0,
+                         (hipStream_t)stream, a, groups, ctx->groupList, ctx->groupCount);
+      HIP_TRY(hipGetLastError());
+      // about one wave per listed group: the benchmark scenes list 13-17 % of
+      // their groups; a wave past the count exits at once, and a scene that
+      // lists more deals up to five groups to each wave
+      size_t persist = groups / 5;
+      if (persist < (size_t)ctx->numCU * 64) persist = (size_t)ctx->numCU * 64;
+      if (ctx->persistPerCU > 0) persist = (size_t)ctx->numCU * ctx->persistPerCU;
+      a.groupList = ctx->groupList;
+      a.groupCount = ctx->groupCount;
+      a.nPersist = (unsigned)(groups < persist ? groups : persist);
+      grid = dim3(a.nPersist, 1);
+    }
   }
   const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * threads * 16;
   const size_t lds = frameLds +

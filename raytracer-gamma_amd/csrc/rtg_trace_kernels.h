@@ -204,14 +204,23 @@ struct DevScene {
   __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
   // |0 - c_i|^2 - r_i^2: the c term of a ray from the origin (primary rays)
   __device__ __forceinline__ float origin_c(unsigned i) const { return crad2[n + i]; }
-  __device__ __forceinline__ Mat mat(int i) const {
-    const auto p = mats + 8 * i;
+  __device__ __forceinline__ Mat mat_at(decltype(mats) p) const {
     Mat r;
     r.matte = v3(p[0], p[1], p[2]);
     r.gloss = v3(p[3], p[4], p[5]);
     r.opacity = p[6];
     r.refr = p[7];
     return r;
+  }
+  // Material record i; when every active lane asks for the same record (the
+  // background for primary misses, one sphere for a coherent wave) it comes
+  // through scalar loads instead of a per-lane gather.
+  __device__ __forceinline__ Mat mat(int i) const {
+    if constexpr (std::is_same<MatPtr, cfloat_p>::value) {
+      const int i0 = __builtin_amdgcn_readfirstlane(i);
+      if (__ballot(i != i0) == 0ull) return mat_at(mats + 8 * i0);
+    }
+    return mat_at(mats + 8 * i);
   }
   __device__ __forceinline__ float refr(int i) const { return mats[8 * i + 7]; }
   __device__ __forceinline__ void light(unsigned l, V3& pos, V3& col) const {
@@ -239,9 +248,42 @@ struct KernelArgs {
   unsigned W, rowsLocal, rowBlock, shard, nShards;
   const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
   float* dst;
+  // Compacted launch (cull_groups_kernel): the pixel groups some primary ray
+  // may hit, their count, and the number of persistent waves; null otherwise.
+  const unsigned* groupList;
+  const unsigned* groupCount;
+  unsigned nPersist;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
   uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
 };
+
+// floor(a / d) for a <= 64, 1 <= d <= 64: (a + 0.5) / d is at least 1/128
+// from an integer, far beyond the float product's error.
+#ifndef RTG_PROBE_FLOOR
+#define RTG_PROBE_FLOOR 0
+#endif
+
+__device__ __forceinline__ unsigned udiv_small(unsigned a, unsigned d) {
+  return (unsigned)(((float)a + 0.5f) * (1.0f / (float)d));
+}
+// q = a / d, r = a % d for a < 2^53, d >= 1: the f64 quotient estimate is
+// within one of the true quotient; one integer correction each way.
+__device__ __forceinline__ void divmod_u64(uint64_t a, unsigned d, unsigned& q, unsigned& r) {
+  uint64_t qq = (uint64_t)((double)a * (1.0 / (double)d));
+  int64_t rr = (int64_t)(a - qq * d);
+  if (rr < 0) { --qq; rr += d; }
+  else if (rr >= (int64_t)d) { ++qq; rr -= d; }
+  q = (unsigned)qq;
+  r = (unsigned)rr;
+}
+// shard_global_row (rtg_internal.h) with the division by the block size done
+// through divmod_u64.
+__device__ __forceinline__ unsigned shard_global_row_fast(unsigned localRow, unsigned B,
+                                                         unsigned g, unsigned G) {
+  unsigned lb, rem;
+  divmod_u64(localRow, B, lb, rem);
+  return (lb * G + g) * B + rem;
+}
 
 __device__ __forceinline__ float canon_nan(float v) {
   // x86 default NaN, what the reference CPU path writes (see rtg.h).
@@ -415,38 +457,40 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned SP = nAA * nAA;
   const unsigned PPW = 64u / SP;
-  const unsigned pl = lane / SP, s = lane - pl * SP;
-  const size_t p = gw * PPW + pl;
+  // No integer divisions by run-time values (each is a ~25-instruction
+  // sequence on the GPU; a trivial wave's whole cost is this set-up): small
+  // quotients through float reciprocals, the wave's first pixel through
+  // divmod_u64, the lanes' rows by carrying from it.
+  const unsigned pl = udiv_small(lane, SP), s = lane - pl * SP;
+  const size_t p0 = gw * PPW;  // the wave's first pixel (wave-uniform)
   const size_t total = (size_t)a.W * a.rowsLocal;
+  const size_t p = p0 + pl;
   const bool valid = pl < PPW && p < total;
-  unsigned x = 0, lr = 0, gy = 0;
-  if (valid) {
-    if (total <= 0xFFFFFFFFull) {  // wave-uniform: 32-bit division
-      lr = (unsigned)p / a.W;
-      x = (unsigned)p - lr * a.W;
-    } else {
-      lr = (unsigned)(p / a.W);
-      x = (unsigned)(p - (size_t)lr * a.W);
-    }
-    gy = a.rowList ? a.rowList[lr] : shard_global_row(lr, a.rowBlock, a.shard, a.nShards);
+  unsigned col0, r0;
+  divmod_u64(p0, a.W, r0, col0);
+  unsigned x = col0 + pl, lr = r0, gy = 0;
+  while (x >= a.W) {  // PPW <= 64 pixels past the first: rarely one row
+    x -= a.W;
+    ++lr;
   }
-  const int si = (int)(s / nAA), sj = (int)(s - (unsigned)si * nAA);
+  if (valid) gy = a.rowList ? a.rowList[lr] : shard_global_row_fast(lr, a.rowBlock, a.shard,
+                                                                    a.nShards);
+  const int si = (int)udiv_small(s, nAA), sj = (int)(s - (unsigned)si * nAA);
   float rx, ry;
   const V3 dir = sample_dir(a.cam, x, gy, si, sj, rx, ry);
 
   // Primary-ray cull over the wave's sample directions (wave converged).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if (a.n <= 64) {
+  if (RTG_PROBE_FLOOR < 2 && a.n <= 64) {
     float x0, x1, y0, y1;
     // Wave-uniform: do the wave's valid pixels lie in one row?  Then the
     // bounds are four lanes' values, since every float step of main.cpp:
     // 419-426 is monotone: rx grows with x and j (lane 0 has the smallest,
     // the last pixel's j = nAA-1 lane the largest) and ry with i (lane 0, and
     // lane nAA(nAA-1)).  Otherwise reduce across the wave.
-    const size_t p0 = gw * PPW;
     const unsigned nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);  // >= 1
-    const bool oneRow = (p0 / a.W) == ((p0 + nv - 1) / a.W);
+    const bool oneRow = col0 + nv - 1 < a.W;
     if (oneRow && !kShfl) {
       x0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rx), 0));
       x1 = __int_as_float(
@@ -480,10 +524,15 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
     for (int k = 0; k < kProbeSlots; ++k) sc.acc[k] = 0;
     tk0 = __builtin_amdgcn_s_memtime();
   }
+#if RTG_PROBE_FLOOR >= 1  // diagnostic builds only (tools/probe_floor.py): no tracing
+  (void)usePrim;
+  c = vsmul(a.cam.inv, v3(dir.x, (float)__builtin_popcountll(primSel), 0.f));
+#else
   if (valid) {
     c = trace_sample<S, Q, kCL>(sc, dir, sc.frames(), usePrim, primSel);
     c = vsmul(a.cam.inv, c);
   }
+#endif
   if constexpr (kDiag) {  // wave converged again: one add per slot
     sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
     if ((threadIdx.x & 63u) == 0)
@@ -527,6 +576,11 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
 }
 
 template <int kVariant>
+struct GroupsPerWave {
+  static constexpr int value = (kVariant == 21) ? 4 : 1;
+};
+
+template <int kVariant>
 struct SampleThreads {
   static constexpr int value = (kVariant == 14) ? kBlock : (kVariant == 16) ? 128 : 64;
 };
@@ -544,15 +598,26 @@ void trace_samples_kernel(const KernelArgs a) {
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screen every sphere)
-  trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
-              (kVariant == 50)>(a, sc, gw);
+  // variant 21: kGroupsPerWave consecutive pixel groups per wave, in turn
+  constexpr int K = GroupsPerWave<kVariant>::value;
+  if (a.groupList) {  // compacted: the listed groups, dealt round-robin to the waves
+    const unsigned cnt = *(const RTG_CONST unsigned*)a.groupCount;
+    for (size_t idx = gw; idx < cnt; idx += a.nPersist)
+      trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
+                  (kVariant == 50)>(a, sc, ((const RTG_CONST unsigned*)a.groupList)[idx]);
+  } else {
+    for (int k = 0; k < K; ++k)
+      trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
+                  (kVariant == 50)>(a, sc, gw * K + k);
+  }
   record_wave(a, t0, gw);
 }
 
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
 //   0 (default) sample-parallel: one primary sample per lane, one-wave
 //     workgroups, scene tables read from global memory (trace_samples_kernel);
-//     falls back to 9 when nAA > 8
+//     compacted launch for scenes of <= 64 spheres (cull_groups_kernel,
+//     rtg_kernel.hip); falls back to 9 when nAA > 8
 //   1 per-sample recursion, one sphere per step (first kernel)
 //   2 one-query-per-iteration state machine + candidate masks
 //   3 one-query-per-iteration state machine, four spheres per step
@@ -569,6 +634,9 @@ void trace_samples_kernel(const KernelArgs a) {
 //   18 as 0 built for 8 waves per SIMD (<= 64 VGPRs)
 //   19 as 0 with shuffle reductions for the cull bounds and the pixel sum
 //   20 as 0 without the secondary-ray cone cull (cone_masks)
+//   21 as 0 with four consecutive pixel groups per wave
+//   22 as 0 without the compacted launch (one wave per pixel group, every
+//      group traced: the default before cull_groups_kernel)
 //   50 / 59: 0 / 9 with the OpenCL kernel's semantics (RTG_SEMANTICS_OPENCL;
 //     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
@@ -594,7 +662,7 @@ constexpr VariantInfo kVariants[] = {
     {6, kVariantTile, false},    {8, kVariantTile, false},    {9, kVariantTile, false},
     {14, kVariantSample, false}, {15, kVariantSample, false}, {16, kVariantSample, false},
     {17, kVariantSample, false}, {18, kVariantSample, false}, {19, kVariantSample, false},
-    {20, kVariantSample, false},
+    {20, kVariantSample, false}, {21, kVariantSample, false}, {22, kVariantSample, false},
     {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
     {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
 };
@@ -608,7 +676,8 @@ template <int S, int V>
 static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 20 || V == 50 || V == 110)
+  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 20 || V == 21 || V == 22 ||
+                     V == 50 || V == 110)
     return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -639,6 +708,8 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh) {
     case 18: return trace_fn_v<S, 18>(lds);
     case 19: return trace_fn_v<S, 19>(lds);
     case 20: return trace_fn_v<S, 20>(lds);
+    case 21: return trace_fn_v<S, 21>(lds);
+    case 22: return trace_fn_v<S, 22>(lds);
     case 50: return trace_fn_v<S, 50>(lds);
     case 59: return trace_fn_v<S, 59>(lds);
     case 104: return trace_fn_v<S, 104>(lds);
