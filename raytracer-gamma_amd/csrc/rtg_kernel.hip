@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 // sample kernel's floor(64 / nAA^2) consecutive pixels).  The group's
 // primary-ray bundle is bounded from primary_bounds of each of its pixels
 // (the extremes of sample_dir's monotone float steps, as trace_group's cull)
-// and tested against every sphere with primary_sphere_possible.  A group no
+// and tested against every sphere with primary_possible.  A group no
 // sphere can be reached from is written directly: every sample misses
 // (closest_hit_sel over an empty set, raytracer.h:454-459), returns
 // I (x) bgMaterial.matte = (1,1,1) (x) 0 = +0 (raytracer.h:544, the
@@ -120,28 +120,35 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     p0 = g * PPW;
     nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);
     unsigned col, lr;
-    divmod_u64(p0, a.W, lr, col);
+    divmod_u64(p0, a.W, a.invW, lr, col);
     float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
+    // one row: the first and last pixels bound the group (monotone float
+    // steps, see trace_group); otherwise every pixel
+    const bool oneRow = col + nv - 1 < a.W;
     for (unsigned k = 0; k < nv; ++k) {
-      const unsigned gy = a.rowList ? a.rowList[lr]
-                                    : shard_global_row_fast(lr, a.rowBlock, a.shard, a.nShards);
-      float bx0, bx1, by0, by1;
-      primary_bounds(a.cam, col, gy, bx0, bx1, by0, by1);
-      x0 = fminf(x0, bx0);
-      x1 = fmaxf(x1, bx1);
-      y0 = fminf(y0, by0);
-      y1 = fmaxf(y1, by1);
+      if (!oneRow || k == 0 || k == nv - 1) {
+        const unsigned gy =
+            a.rowList ? a.rowList[lr]
+                      : shard_global_row_fast(lr, a.rowBlock, a.invRowBlock, a.shard, a.nShards);
+        float bx0, bx1, by0, by1;
+        primary_bounds(a.cam, col, gy, bx0, bx1, by0, by1);
+        x0 = fminf(x0, bx0);
+        x1 = fmaxf(x1, bx1);
+        y0 = fminf(y0, by0);
+        y1 = fmaxf(y1, by1);
+      }
       if (++col == a.W) {
         col = 0;
         ++lr;
       }
     }
+    const PrimBundle pb = primary_bundle(x0, x1, y0, y1, a.cam.zoom);
     const RTG_CONST float* geom = (const RTG_CONST float*)a.geom;
+    const RTG_CONST float* pc = (const RTG_CONST float*)a.prim;
     for (unsigned i = 0; i < a.n; ++i) {  // wave-uniform: scalar sphere records
       const RTG_CONST float* r = geom + 4 * i;
-      possible = possible ||
-                 primary_sphere_possible(v3(r[0], r[1], r[2]), sqrtf(r[3]), x0, x1, y0, y1,
-                                         a.cam.zoom);
+      const RTG_CONST float* k = pc + 4 * i;
+      possible |= primary_possible(pb, v3(r[0], r[1], r[2]), k[0], k[1], k[2]);
     }
   }
   if (g < nGroups && !possible) {
@@ -183,6 +190,7 @@ struct rtg_context {
   float* lights = nullptr;
   unsigned* smask = nullptr;  // shadow masks (null when the scene has none)
   unsigned* cone = nullptr;   // secondary-ray cone masks (null when none)
+  float* prim = nullptr;      // primary-cull sphere constants
   float* bvhNodes = nullptr;  // BVH (null when the scene has none)
   float* bvhAux = nullptr;
   int* bvhChild = nullptr;
@@ -210,6 +218,8 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->smask);
   (void)hipFree(c->cone);
   c->cone = nullptr;
+  (void)hipFree(c->prim);
+  c->prim = nullptr;
   (void)hipFree(c->bvhNodes);
   (void)hipFree(c->bvhAux);
   (void)hipFree(c->bvhChild);
@@ -417,6 +427,13 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->smask, ps.smask.data(), ps.smask.size() * sizeof(unsigned),
                       hipMemcpyHostToDevice));
   }
+  if (hipMalloc(&ctx->prim, ps.prim.size() * sizeof(float)) != hipSuccess) {
+    free_scene(ctx);
+    rtg_set_error("hipMalloc failed for the primary-cull constants");
+    return RTG_ERR_NOMEM;
+  }
+  HIP_TRY(hipMemcpy(ctx->prim, ps.prim.data(), ps.prim.size() * sizeof(float),
+                    hipMemcpyHostToDevice));
   if (!ps.cone.empty()) {
     if (hipMalloc(&ctx->cone, ps.cone.size() * sizeof(unsigned)) != hipSuccess) {
       free_scene(ctx);
@@ -510,6 +527,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.lights = ctx->lights;
   a.smask = ctx->smask;
   a.cone = ctx->cone;
+  a.prim = ctx->prim;
   a.bvhNodes = ctx->bvhNodes;
   a.bvhAux = ctx->bvhAux;
   a.bvhChild = ctx->bvhChild;
@@ -519,6 +537,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.W = width;
   a.rowsLocal = rows;
   a.rowBlock = rowBlock ? rowBlock : 1;
+  a.invW = 1.0 / (double)width;
+  a.invRowBlock = 1.0 / (double)a.rowBlock;
   a.shard = shard;
   a.nShards = nShards ? nShards : 1;
   a.rowList = rowList;

@@ -39,6 +39,8 @@ constexpr unsigned kMaskMaxSpheres = 64;
 // lights: m x {pos.xyz, col.xyz}.  Arrays are never empty (padded to 1).
 struct PackedScene {
   std::vector<float> geom, crad2, mats, lights;
+  // Primary-cull sphere constants (prim_consts): n x {1/|c|, sin a, cos a, 0}.
+  std::vector<float> prim;
   // Sphere masks (shadow_masks below): m x n shadow masks, then n overlap
   // masks, each {lo, hi} words, for 1 <= n <= 64 and a finite scene; empty
   // otherwise (every sphere is then tested).
@@ -107,6 +109,29 @@ inline double contain_reach(const rtg_sphere& s) {
   const double g = guard_radius(s);
   const double c = fabs((double)s.pos.x) + fabs((double)s.pos.y) + fabs((double)s.pos.z);
   return g + 0.01 * (double)kContainDirMax * (1.0 + 0x1p-16) + 0x1p-16 * (c + g + 1.0);
+}
+
+// The sphere half of the primary-ray cull (primary_possible, rtg_trace.h):
+// seen from the camera origin, sphere c, r with the radius inflated to
+// rr = |r| * 1.001 + 1e-3 has angular radius alpha, sin(alpha) = rr / |c|.
+// Computed in double and rounded (the test's 2e-3 margin dwarfs that);
+// cos(alpha) = -3, sin(alpha) = 0 mark "always possible" (sin(alpha) >= 0.999:
+// the origin inside or near the sphere; or a non-finite or zero centre).
+inline void prim_consts(const rtg_sphere& s, float* out) {
+  const double cx = s.pos.x, cy = s.pos.y, cz = s.pos.z;
+  const double L = sqrt(cx * cx + cy * cy + cz * cz);
+  const double rr = fabs((double)s.radius) * 1.001 + 1e-3;
+  const double sa = rr / L;
+  out[3] = 0.f;
+  if (!(sa < 0.999) || !(L > 0.0) || !(L < 1e30)) {
+    out[0] = 0.f;
+    out[1] = 0.f;
+    out[2] = -3.f;
+    return;
+  }
+  out[0] = (float)(1.0 / L);
+  out[1] = (float)sa;
+  out[2] = (float)sqrt(1.0 - sa * sa);
 }
 
 inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
@@ -425,6 +450,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   ps->crad2.assign(n ? 3 * (size_t)n : 1, 0.f);
   ps->mats.assign((size_t)(n + 1) * 8, 0.f);
   ps->lights.assign((size_t)(m ? m : 1) * 6, 0.f);
+  ps->prim.assign((size_t)(n ? n : 1) * 4, 0.f);
   for (unsigned i = 0; i < n; ++i) {
     const rtg_sphere& s = spheres[i];
     float* g = &ps->geom[(size_t)i * 4];
@@ -441,6 +467,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     const float dx = 0.f - s.pos.x, dy = 0.f - s.pos.y, dz = 0.f - s.pos.z;
     ps->crad2[n + i] = (((dx * dx) + (dy * dy)) + (dz * dz)) - g[3];
     ps->crad2[2 * (size_t)n + i] = guard_r2(s);
+    prim_consts(s, &ps->prim[(size_t)i * 4]);
     float* mt = &ps->mats[(size_t)i * 8];
     mt[0] = s.material.matteColour.x; mt[1] = s.material.matteColour.y;
     mt[2] = s.material.matteColour.z; mt[3] = s.material.glossColour.x;

@@ -130,7 +130,7 @@ RTG_HD float rcp_rn(float b) {
   return y;
 }
 // Approximate reciprocal square root (v_rsq_f32, ~1 ulp) for conservative
-// culls only (primary_sphere_possible, the cone cull); never for results.
+// culls only (primary_bundle, the cone cull); never for results.
 RTG_HD float cull_rsq(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_rsqf(x);
@@ -1274,30 +1274,45 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
 // Bundles wider than 60 degrees, and spheres at or around the origin, are
 // never culled.
 
-RTG_HD bool primary_sphere_possible(V3 c, float r, float x0, float x1, float y0, float y1,
-                                    float zoom) {
-  if (!(zoom != 0.f)) return true;
+// The bundle half of the test: axis U, cos(theta) and sin(theta) of the
+// bundle's half-angle, or `all` (no cull) for wide or degenerate bundles.
+struct PrimBundle {
+  V3 U;
+  float cosT, st;
+  bool all;
+};
+RTG_HD PrimBundle primary_bundle(float x0, float x1, float y0, float y1, float zoom) {
+  PrimBundle b;
+  b.all = true;
+  b.U = v3(0.f, 0.f, 0.f);
+  b.cosT = 1.f;
+  b.st = 0.f;
+  if (!(zoom != 0.f)) return b;
   const float xc = 0.5f * (x0 + x1), yc = 0.5f * (y0 + y1);
   const float ila = cull_rsq(xc * xc + yc * yc + zoom * zoom);
-  const V3 U = v3(xc * ila, yc * ila, zoom * ila);
+  b.U = v3(xc * ila, yc * ila, zoom * ila);
   float cosT = 1.f;
   const float xs[2] = {x0, x1}, ys[2] = {y0, y1};
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) {
-      const float il = cull_rsq(xs[a] * xs[a] + ys[b] * ys[b] + zoom * zoom);
-      cosT = fminf(cosT, (U.x * xs[a] + U.y * ys[b] + U.z * zoom) * il);
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) {
+      const float il = cull_rsq(xs[i] * xs[i] + ys[j] * ys[j] + zoom * zoom);
+      cosT = fminf(cosT, (b.U.x * xs[i] + b.U.y * ys[j] + b.U.z * zoom) * il);
     }
-  if (!(cosT >= 0.5f)) return true;  // wide (or NaN) bundle
-  const float L2 = vdot(c, c);
-  const float iL = cull_rsq(L2);
-  const float rr = r * 1.001f + 1.0e-3f;
-  const float sa = rr * iL;  // sin(alpha)
-  if (!(sa < 0.999f)) return true;  // origin inside or near the sphere (or NaN)
-  const float ca2 = 1.f - sa * sa, st2 = fmaxf(0.f, 1.f - cosT * cosT);
-  const float ca = ca2 * cull_rsq(ca2);
-  const float st = st2 > 0.f ? st2 * cull_rsq(st2) : 0.f;
-  const float cosLim = cosT * ca - st * sa;  // theta + alpha < 60 + 90 degrees
-  const float cosPhi = vdot(U, c) * iL;
+  if (!(cosT >= 0.5f)) return b;  // wide (or NaN) bundle
+  const float st2 = fmaxf(0.f, 1.f - cosT * cosT);
+  b.cosT = cosT;
+  b.st = st2 > 0.f ? st2 * cull_rsq(st2) : 0.f;
+  b.all = false;
+  return b;
+}
+// The sphere half: {1/|c|, sin(alpha), cos(alpha)} of sphere c, r, with the
+// radius inflated to r * 1.001 + 1e-3, computed once per scene on the host
+// (prim_consts, rtg_scene_pack.h; cos(alpha) = -3 for "always possible":
+// the origin inside or near the sphere, or a non-finite sphere).
+RTG_HD bool primary_possible(const PrimBundle& b, V3 c, float iL, float sa, float ca) {
+  if (b.all) return true;
+  const float cosLim = b.cosT * ca - b.st * sa;  // theta + alpha < 60 + 90 degrees
+  const float cosPhi = vdot(b.U, c) * iL;
   return cosPhi >= cosLim - 2.0e-3f;
 }
 

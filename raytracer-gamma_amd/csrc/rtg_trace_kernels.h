@@ -82,6 +82,7 @@ struct DevScene {
   cfloat_p lights;
   cuint_p smask;  // m x n x {lo, hi} shadow masks, or null
   cuint_p cone;   // n x kConeCells x {lo, hi} secondary-ray cone masks, or null
+  cfloat_p prim;  // n x {1/|c|, sin a, cos a, 0}: primary-cull sphere constants
   cfloat_p bvhNodes;  // BVH (build_bvh, rtg_scene_pack.h) or null
   int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
   cfloat_p bvhAux;
@@ -202,6 +203,11 @@ struct DevScene {
     return v3(g.x, g.y, g.z);
   }
   __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
+  // primary_possible's per-sphere constants of sphere i
+  __device__ __forceinline__ bool prim_possible(const PrimBundle& b, unsigned i, V3 c) const {
+    const cfloat_p k = prim + 4 * i;
+    return primary_possible(b, c, k[0], k[1], k[2]);
+  }
   // |0 - c_i|^2 - r_i^2: the c term of a ray from the origin (primary rays)
   __device__ __forceinline__ float origin_c(unsigned i) const { return crad2[n + i]; }
   __device__ __forceinline__ Mat mat_at(decltype(mats) p) const {
@@ -240,12 +246,14 @@ struct KernelArgs {
   const float* lights;
   const unsigned* smask;  // shadow masks (PackedScene::smask) or null
   const unsigned* cone;   // cone masks (PackedScene::cone) or null
+  const float* prim;      // primary-cull sphere constants (PackedScene::prim)
   const float* bvhNodes;  // BVH (PackedScene::bvh*) or null
   const float* bvhAux;
   const int* bvhChild;
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
+  double invW, invRowBlock;  // RN(1.0 / W), RN(1.0 / rowBlock) (divmod_u64)
   const unsigned* rowList;  // explicit global rows (rtg_render_rows_device) or null
   float* dst;
   // Compacted launch (cull_groups_kernel): the pixel groups some primary ray
@@ -266,10 +274,12 @@ struct KernelArgs {
 __device__ __forceinline__ unsigned udiv_small(unsigned a, unsigned d) {
   return (unsigned)(((float)a + 0.5f) * (1.0f / (float)d));
 }
-// q = a / d, r = a % d for a < 2^53, d >= 1: the f64 quotient estimate is
-// within one of the true quotient; one integer correction each way.
-__device__ __forceinline__ void divmod_u64(uint64_t a, unsigned d, unsigned& q, unsigned& r) {
-  uint64_t qq = (uint64_t)((double)a * (1.0 / (double)d));
+// q = a / d, r = a % d for a < 2^53, d >= 1, invd = RN(1.0 / d) (host): the
+// f64 quotient estimate is within one of the true quotient; one integer
+// correction each way.
+__device__ __forceinline__ void divmod_u64(uint64_t a, unsigned d, double invd, unsigned& q,
+                                           unsigned& r) {
+  uint64_t qq = (uint64_t)((double)a * invd);
   int64_t rr = (int64_t)(a - qq * d);
   if (rr < 0) { --qq; rr += d; }
   else if (rr >= (int64_t)d) { ++qq; rr -= d; }
@@ -279,9 +289,9 @@ __device__ __forceinline__ void divmod_u64(uint64_t a, unsigned d, unsigned& q, 
 // shard_global_row (rtg_internal.h) with the division by the block size done
 // through divmod_u64.
 __device__ __forceinline__ unsigned shard_global_row_fast(unsigned localRow, unsigned B,
-                                                         unsigned g, unsigned G) {
+                                                         double invB, unsigned g, unsigned G) {
   unsigned lb, rem;
-  divmod_u64(localRow, B, lb, rem);
+  divmod_u64(localRow, B, invB, lb, rem);
   return (lb * G + g) * B + rem;
 }
 
@@ -327,6 +337,7 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.lights = (cfloat_p)a.lights;
   sc.smask = (cuint_p)a.smask;
   sc.cone = (cuint_p)a.cone;
+  sc.prim = (cfloat_p)a.prim;
   sc.bvhNodes = (cfloat_p)a.bvhNodes;
   // BVH scenes: 64 stack entries per wave after the frames and scene tables
   // (the launcher adds them to the LDS size).
@@ -356,7 +367,7 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
 
   // Primary-ray sphere cull for this wave (whole wave converged here): the
   // bounds of every sample direction of the wave's pixels, then one sphere
-  // per lane against that bundle, then a ballot (see primary_sphere_possible).
+  // per lane against that bundle, then a ballot (see primary_possible).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
   if constexpr (kBase == 0 || kBase == 8 || kBase == 9 || kBase == 59) {
@@ -369,11 +380,11 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
         y0 = fminf(y0, __shfl_xor(y0, off));
         y1 = fmaxf(y1, __shfl_xor(y1, off));
       }
+      const PrimBundle pb = primary_bundle(x0, x1, y0, y1, a.cam.zoom);
       bool possible = false;
       if (lane < a.n) {
         const float4 g = sc.lgeom[lane];
-        possible = primary_sphere_possible(v3(g.x, g.y, g.z), sqrtf(g.w), x0, x1, y0, y1,
-                                           a.cam.zoom);
+        possible = sc.prim_possible(pb, lane, v3(g.x, g.y, g.z));
       }
       primSel = __ballot(possible);
       usePrim = true;
@@ -467,14 +478,15 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   const size_t p = p0 + pl;
   const bool valid = pl < PPW && p < total;
   unsigned col0, r0;
-  divmod_u64(p0, a.W, r0, col0);
+  divmod_u64(p0, a.W, a.invW, r0, col0);
   unsigned x = col0 + pl, lr = r0, gy = 0;
   while (x >= a.W) {  // PPW <= 64 pixels past the first: rarely one row
     x -= a.W;
     ++lr;
   }
-  if (valid) gy = a.rowList ? a.rowList[lr] : shard_global_row_fast(lr, a.rowBlock, a.shard,
-                                                                    a.nShards);
+  if (valid)
+    gy = a.rowList ? a.rowList[lr]
+                   : shard_global_row_fast(lr, a.rowBlock, a.invRowBlock, a.shard, a.nShards);
   const int si = (int)udiv_small(s, nAA), sj = (int)(s - (unsigned)si * nAA);
   float rx, ry;
   const V3 dir = sample_dir(a.cam, x, gy, si, sj, rx, ry);
@@ -509,11 +521,11 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
         y1 = fmaxf(y1, __shfl_xor(y1, off));
       }
     }
+    const PrimBundle pb = primary_bundle(x0, x1, y0, y1, a.cam.zoom);
     bool possible = false;
     if (lane < a.n) {
       const float4 g = sc.lgeom[lane];
-      possible = primary_sphere_possible(v3(g.x, g.y, g.z), sqrtf(g.w), x0, x1, y0, y1,
-                                         a.cam.zoom);
+      possible = sc.prim_possible(pb, lane, v3(g.x, g.y, g.z));
     }
     primSel = __ballot(possible);
     usePrim = true;

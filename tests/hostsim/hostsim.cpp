@@ -33,6 +33,7 @@ struct HostScene {
   const float* bvhAux = nullptr;
   const int* bvhChild = nullptr;
   bool has_bvh() const { return bvhNodes != nullptr; }
+  const float* prim = nullptr;
   const unsigned* cone = nullptr;
   bool has_cone() const { return cone != nullptr; }
   rtg::V3 first_lane(rtg::V3 v) const { return v; }
@@ -153,12 +154,13 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
         if (use) {
           float x0, x1, y0, y1;
           rtg::primary_bounds(cam, x, y, x0, x1, y0, y1);
+          const rtg::PrimBundle pb = rtg::primary_bundle(x0, x1, y0, y1, cam.zoom);
           sel = 0;
           for (unsigned k = 0; k < sc.n; ++k) {
             float r2;
             const rtg::V3 c = sc.sphere(k, r2);
-            if (rtg::primary_sphere_possible(c, sqrtf(r2), x0, x1, y0, y1, cam.zoom))
-              sel |= 1ull << k;
+            const float* pk = sc.prim + 4 * k;
+            if (rtg::primary_possible(pb, c, pk[0], pk[1], pk[2])) sel |= 1ull << k;
           }
         }
         p = rtg::shade_pixel<S, 2, true>(sc, cam, x, y, use, sel);
@@ -195,6 +197,7 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   HostScene sc{ps.geom.data(), ps.crad2.data(), ps.mats.data(), ps.lights.data(), n, m, ps.n4};
   sc.smask = ps.smask.empty() ? nullptr : ps.smask.data();
   sc.cone = ps.cone.empty() ? nullptr : ps.cone.data();
+  sc.prim = ps.prim.data();
   if (!ps.bvhChild.empty() && g_useBvh) {
     sc.bvhNodes = ps.bvhNodes.data();
     sc.bvhAux = ps.bvhAux.data();
@@ -212,7 +215,8 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   return 0;
 }
 
-// Conservativeness of the primary-ray cull (primary_sphere_possible): over
+// Conservativeness of the primary-ray cull (primary_bundle + primary_possible
+// with the host's prim_consts): over
 // every group of `group` consecutive pixels of a W x H frame (the sample
 // kernel's wave), bound the group's sample directions as the kernel does,
 // then count spheres the cull drops although one of those samples hits them
@@ -236,10 +240,12 @@ extern "C" long hostsim_cull_violations(const rtg_sphere* spheres, unsigned n, u
           rtg::sample_dir(cam, (unsigned)(p % W), (unsigned)(p / W), i, j, rx, ry);
           x0 = fminf(x0, rx); x1 = fmaxf(x1, rx); y0 = fminf(y0, ry); y1 = fmaxf(y1, ry);
         }
+    const rtg::PrimBundle pb = rtg::primary_bundle(x0, x1, y0, y1, cam.zoom);
     for (unsigned k = 0; k < n; ++k) {
       float r2;
       const rtg::V3 c = sc.sphere(k, r2);
-      if (rtg::primary_sphere_possible(c, sqrtf(r2), x0, x1, y0, y1, cam.zoom)) continue;
+      const float* pk = &ps.prim[(size_t)k * 4];
+      if (rtg::primary_possible(pb, c, pk[0], pk[1], pk[2])) continue;
       ++drop;
       for (size_t p = p0; p < p0 + group && p < total; ++p)
         for (int i = 0; i < cam.nAA; ++i)

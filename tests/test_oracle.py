@@ -196,7 +196,7 @@ def test_kernel_traversal_c1_full_frame(hostsim, variant, golden):
 
 @pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
 def test_primary_cull_is_conservative(hostsim, golden, name):
-    """primary_sphere_possible never drops a sphere that a sample of the
+    """The primary cull (primary_bundle + primary_possible) never drops a sphere that a sample of the
     bundle hits (exact root test), over whole small frames of every config,
     for the sample kernel's 7-pixel groups and the tile kernel's rows."""
     c = golden["configs"][name]
