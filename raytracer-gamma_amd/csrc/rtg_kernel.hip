@@ -100,71 +100,102 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 // primary-ray bundle is bounded from primary_bounds of each of its pixels
 // (the extremes of sample_dir's monotone float steps, as trace_group's cull)
 // and tested against every sphere with primary_possible.  A group no
-// sphere can be reached from is written directly: every sample misses
+// sphere can be reached from is written +0 directly: every sample misses
 // (closest_hit_sel over an empty set, raytracer.h:454-459), returns
 // I (x) bgMaterial.matte = (1,1,1) (x) 0 = +0 (raytracer.h:544, the
 // background matte is 0), and the pixel sum of +0 * inv is +0 in every
 // channel.  The other groups are appended to groupList (one atomic per wave)
 // for the trace kernel.  n <= 64 spheres.
+// Whether pixel group g can reach a sphere (the cull of trace_group).
+__device__ __forceinline__ bool group_live(const KernelArgs& a, size_t g, unsigned PPW,
+                                           size_t total) {
+  const size_t p0 = g * PPW;
+  const unsigned nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);
+  unsigned col, lr;
+  divmod_u64(p0, a.W, a.invW, lr, col);
+  float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
+  // one row: the first and last pixels bound the group (monotone float
+  // steps, see trace_group); otherwise every pixel
+  const bool oneRow = col + nv - 1 < a.W;
+  for (unsigned k = 0; k < nv; ++k) {
+    if (!oneRow || k == 0 || k == nv - 1) {
+      const unsigned gy =
+          a.rowList ? a.rowList[lr]
+                    : shard_global_row_fast(lr, a.rowBlock, a.invRowBlock, a.shard, a.nShards);
+      float bx0, bx1, by0, by1;
+      primary_bounds(a.cam, col, gy, bx0, bx1, by0, by1);
+      x0 = fminf(x0, bx0);
+      x1 = fmaxf(x1, bx1);
+      y0 = fminf(y0, by0);
+      y1 = fmaxf(y1, by1);
+    }
+    if (++col == a.W) {
+      col = 0;
+      ++lr;
+    }
+  }
+  const PrimBundle pb = primary_bundle(x0, x1, y0, y1, a.cam.zoom);
+  const RTG_CONST float* geom = (const RTG_CONST float*)a.geom;
+  const RTG_CONST float* pc = (const RTG_CONST float*)a.prim;
+  bool possible = false;
+  for (unsigned i = 0; i < a.n; ++i) {  // wave-uniform: scalar sphere records
+    const RTG_CONST float* r = geom + 4 * i;
+    const RTG_CONST float* k = pc + 4 * i;
+    possible |= primary_possible(pb, v3(r[0], r[1], r[2]), k[0], k[1], k[2]);
+  }
+  return possible;
+}
+
+// A block takes kCullGroups = 4 x 256 consecutive groups (one per lane per
+// round) and appends its live ones with ONE atomic: the atomics on the single
+// counter serialise in L2, so one per wave cost ~70 us on C3.
+constexpr unsigned kCullRounds = 4;
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
                                                           unsigned* groupCount) {
-  const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ unsigned cnt[kCullRounds][4];
+  __shared__ unsigned blockBase;
+  const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned PPW = 64u / (nAA * nAA);
   const size_t total = (size_t)a.W * a.rowsLocal;
-  bool possible = false;
-  size_t p0 = 0;
-  unsigned nv = 0;
-  if (g < nGroups) {
-    p0 = g * PPW;
-    nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);
-    unsigned col, lr;
-    divmod_u64(p0, a.W, a.invW, lr, col);
-    float x0 = 3.0e38f, x1 = -3.0e38f, y0 = 3.0e38f, y1 = -3.0e38f;
-    // one row: the first and last pixels bound the group (monotone float
-    // steps, see trace_group); otherwise every pixel
-    const bool oneRow = col + nv - 1 < a.W;
-    for (unsigned k = 0; k < nv; ++k) {
-      if (!oneRow || k == 0 || k == nv - 1) {
-        const unsigned gy =
-            a.rowList ? a.rowList[lr]
-                      : shard_global_row_fast(lr, a.rowBlock, a.invRowBlock, a.shard, a.nShards);
-        float bx0, bx1, by0, by1;
-        primary_bounds(a.cam, col, gy, bx0, bx1, by0, by1);
-        x0 = fminf(x0, bx0);
-        x1 = fmaxf(x1, bx1);
-        y0 = fminf(y0, by0);
-        y1 = fmaxf(y1, by1);
-      }
-      if (++col == a.W) {
-        col = 0;
-        ++lr;
-      }
+  const size_t blockG = (size_t)blockIdx.x * (256 * kCullRounds);
+  uint64_t live[kCullRounds];
+#pragma unroll
+  for (unsigned k = 0; k < kCullRounds; ++k) {
+    const size_t g = blockG + k * 256 + threadIdx.x;
+    const bool possible = g < nGroups && group_live(a, g, PPW, total);
+    // Zero-fill the pixels of all this wave's groups with coalesced stores
+    // (the trace kernel, later on the same stream, overwrites the live ones).
+    const size_t wg0 = g - lane;  // the wave's first group this round
+    if (wg0 < nGroups) {
+      const size_t q0 = wg0 * PPW * 3;
+      size_t q1 = (wg0 + 64) * PPW * 3;
+      if (q1 > total * 3) q1 = total * 3;
+      for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
     }
-    const PrimBundle pb = primary_bundle(x0, x1, y0, y1, a.cam.zoom);
-    const RTG_CONST float* geom = (const RTG_CONST float*)a.geom;
-    const RTG_CONST float* pc = (const RTG_CONST float*)a.prim;
-    for (unsigned i = 0; i < a.n; ++i) {  // wave-uniform: scalar sphere records
-      const RTG_CONST float* r = geom + 4 * i;
-      const RTG_CONST float* k = pc + 4 * i;
-      possible |= primary_possible(pb, v3(r[0], r[1], r[2]), k[0], k[1], k[2]);
-    }
+    live[k] = __ballot(possible);
+    if (lane == 0) cnt[k][wave] = (unsigned)__builtin_popcountll(live[k]);
   }
-  if (g < nGroups && !possible) {
-    float* o = a.dst + p0 * 3;
-    for (unsigned k = 0; k < nv * 3; ++k) o[k] = 0.f;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned sum = 0;
+    for (unsigned k = 0; k < kCullRounds; ++k)
+      for (unsigned w = 0; w < 4; ++w) sum += cnt[k][w];
+    blockBase = sum ? atomicAdd(groupCount, sum) : 0u;
   }
-  const bool append = g < nGroups && possible;
-  const uint64_t m = __ballot(append);
-  if (m) {
-    const unsigned lane = threadIdx.x & 63u;
-    const int leader = __builtin_ctzll(m);
-    unsigned base = 0;
-    if ((int)lane == leader) base = atomicAdd(groupCount, (unsigned)__builtin_popcountll(m));
-    base = __builtin_amdgcn_readlane(base, leader);
-    if (append) groupList[base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] = (unsigned)g;
+  __syncthreads();
+  unsigned off = blockBase;  // list order: (round, wave, lane)
+#pragma unroll
+  for (unsigned k = 0; k < kCullRounds; ++k) {
+    for (unsigned w = 0; w < 4; ++w)
+      if (w < wave) off += cnt[k][w];
+    const uint64_t m = live[k];
+    if ((m >> lane) & 1ull)
+      groupList[off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
+          (unsigned)(blockG + k * 256 + threadIdx.x);
+    for (unsigned w = wave; w < 4; ++w) off += cnt[k][w];
   }
 }
 
@@ -197,9 +228,18 @@ struct rtg_context {
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
-  unsigned* groupList = nullptr;  // compacted launch: listed pixel groups
-  unsigned* groupCount = nullptr;
-  size_t groupCap = 0;
+  // Compacted-launch scratch: a ring of slots, so that renders of one
+  // context on different streams can overlap; a slot is reused only after
+  // the event recorded behind its last trace kernel.
+  struct GroupSlot {
+    unsigned* list = nullptr;  // listed pixel groups
+    unsigned* count = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+  };
+  static constexpr int kSlots = 4;
+  GroupSlot slots[kSlots];
+  int nextSlot = 0;
   int numCU = 256;
   int persistPerCU = 0;  // > 0: fixed persistent waves per CU (RTG_PERSIST_PER_CU A/B knob)
   size_t timelineCap = 0, timelineCount = 0;
@@ -326,8 +366,11 @@ int rtg_context_destroy(rtg_context* ctx) {
   (void)hipFree(ctx->maxScratch);
   (void)hipFree(ctx->diag);
   (void)hipFree(ctx->timeline);
-  (void)hipFree(ctx->groupList);
-  (void)hipFree(ctx->groupCount);
+  for (auto& sl : ctx->slots) {
+    (void)hipFree(sl.list);
+    (void)hipFree(sl.count);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
   delete ctx;
   return RTG_OK;
 }
@@ -557,6 +600,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   }
   unsigned threads = (unsigned)kBlock;
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
+  rtg_context::GroupSlot* slot = nullptr;  // compacted launch scratch
   if (sampleKernel) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
     const size_t groupsPerWave = variant == 21 ? 4 : 1;
@@ -576,17 +620,24 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     // one-wave workgroups traces the listed groups round-robin.
     const bool compact = tpb == 64 && variant != 21 && variant != 22;
     if (compact && ctx->n <= 64 && groups <= 0xFFFFFFFFull) {
-      if (ctx->groupCap < groups) {
-        (void)hipFree(ctx->groupList);
-        ctx->groupList = nullptr;
-        ctx->groupCap = 0;
-        HIP_TRY(hipMalloc(&ctx->groupList, groups * sizeof(unsigned)));
-        ctx->groupCap = groups;
+      slot = &ctx->slots[ctx->nextSlot];
+      ctx->nextSlot = (ctx->nextSlot + 1) % rtg_context::kSlots;
+      if (!slot->done) HIP_TRY(hipEventCreateWithFlags(&slot->done, hipEventDisableTiming));
+      else HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, slot->done, 0));
+      if (slot->cap < groups) {
+        // the slot's last kernel must be done before its list is freed
+        HIP_TRY(hipEventSynchronize(slot->done));
+        (void)hipFree(slot->list);
+        slot->list = nullptr;
+        slot->cap = 0;
+        HIP_TRY(hipMalloc(&slot->list, groups * sizeof(unsigned)));
+        slot->cap = groups;
       }
-      if (!ctx->groupCount) HIP_TRY(hipMalloc(&ctx->groupCount, sizeof(unsigned)));
-      HIP_TRY(hipMemsetAsync(ctx->groupCount, 0, sizeof(unsigned), (hipStream_t)stream));
-      hipLaunchKernelGGL(cull_groups_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0,
-                         (hipStream_t)stream, a, groups, ctx->groupList, ctx->groupCount);
+      if (!slot->count) HIP_TRY(hipMalloc(&slot->count, sizeof(unsigned)));
+      HIP_TRY(hipMemsetAsync(slot->count, 0, sizeof(unsigned), (hipStream_t)stream));
+      hipLaunchKernelGGL(cull_groups_kernel,
+                         dim3((unsigned)((groups + 256 * kCullRounds - 1) / (256 * kCullRounds))),
+                         dim3(256), 0, (hipStream_t)stream, a, groups, slot->list, slot->count);
       HIP_TRY(hipGetLastError());
       // about one wave per listed group: the benchmark scenes list 13-17 % of
       // their groups; a wave past the count exits at once, and a scene that
@@ -594,8 +645,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       size_t persist = groups / 5;
       if (persist < (size_t)ctx->numCU * 64) persist = (size_t)ctx->numCU * 64;
       if (ctx->persistPerCU > 0) persist = (size_t)ctx->numCU * ctx->persistPerCU;
-      a.groupList = ctx->groupList;
-      a.groupCount = ctx->groupCount;
+      a.groupList = slot->list;
+      a.groupCount = slot->count;
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
       grid = dim3(a.nPersist, 1);
     }
@@ -619,6 +670,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   }
   hipLaunchKernelGGL(fn, grid, dim3(threads), lds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());
+  if (slot) HIP_TRY(hipEventRecord(slot->done, (hipStream_t)stream));
   return RTG_OK;
 }
 
