@@ -304,9 +304,9 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
 }
 
 // 4-wide BVH of bounding spheres (the queries are closest_bvh, blocked_bvh
-// and container_bvh in rtg_trace.h).  Top-down: a node's spheres are split at
-// the median of the longest centroid axis, and each half again, into four
-// groups; a group of one sphere becomes a sphere slot, a larger group a child
+// and container_bvh in rtg_trace.h).  Top-down: a node's spheres are split in
+// two by a surface-area-style sweep (split below), and each half again, into
+// four groups; a group of one sphere becomes a sphere slot, a larger group a child
 // node; nodes of <= 4 spheres hold sphere slots only.  Bounds are computed in
 // double about the float-rounded centre C of the group's box:
 //   R  = max |c_i - C| + |r_i|            (screen: bound_r2(R (1 + 2^-20)))
@@ -348,15 +348,56 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
       if (mx[a] - mn[a] > mx[ax] - mn[ax]) ax = a;
     return ax;
   };
-  auto split = [&](unsigned lo, unsigned hi) {  // median split of idx[lo, hi)
-    const int ax = longest(lo, hi);
-    const unsigned mid = lo + (hi - lo) / 2;
-    std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi,
-                     [&](unsigned a, unsigned b) {
-                       const double ca = cen(a, ax), cb = cen(b, ax);
-                       return ca < cb || (ca == cb && a < b);
-                     });
-    return mid;
+  // Split of idx[lo, hi) (>= 2 spheres) into two non-empty runs, returned as
+  // the first index of the second run.  Sweeps the centroid order on each
+  // axis and minimises n_left * d_left^2 + n_right * d_right^2, d the half
+  // diagonal of a side's sphere box: the chance that a line passes a node's
+  // bounding sphere grows with its radius squared.
+  std::vector<double> sufD;
+  auto split = [&](unsigned lo, unsigned hi) {
+    const unsigned cnt = hi - lo;
+    double bestCost = 1e308;
+    int bestAx = longest(lo, hi);
+    unsigned bestK = cnt / 2;
+    sufD.assign(cnt + 1, 0.0);
+    for (int ax = 0; ax < 3; ++ax) {
+      std::sort(idx.begin() + lo, idx.begin() + hi, [&](unsigned a, unsigned b) {
+        const double ca = cen(a, ax), cb = cen(b, ax);
+        return ca < cb || (ca == cb && a < b);
+      });
+      auto box = [&](unsigned i, double* mn, double* mx) {
+        const double r = fabs((double)spheres[i].radius);
+        for (int q = 0; q < 3; ++q) {
+          mn[q] = fmin(mn[q], cen(i, q) - r);
+          mx[q] = fmax(mx[q], cen(i, q) + r);
+        }
+      };
+      auto diag2 = [](const double* mn, const double* mx) {
+        double d = 0.0;
+        for (int q = 0; q < 3; ++q) d += 0.25 * (mx[q] - mn[q]) * (mx[q] - mn[q]);
+        return d;
+      };
+      double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+      for (unsigned k = cnt; k-- > 1;) {  // suffix boxes: runs [k, cnt)
+        box(idx[lo + k], mn, mx);
+        sufD[k] = diag2(mn, mx);
+      }
+      double pmn[3] = {1e300, 1e300, 1e300}, pmx[3] = {-1e300, -1e300, -1e300};
+      for (unsigned k = 1; k < cnt; ++k) {  // prefix [0, k) | suffix [k, cnt)
+        box(idx[lo + k - 1], pmn, pmx);
+        const double cost = k * diag2(pmn, pmx) + (cnt - k) * sufD[k];
+        if (cost < bestCost) {
+          bestCost = cost;
+          bestAx = ax;
+          bestK = k;
+        }
+      }
+    }
+    std::sort(idx.begin() + lo, idx.begin() + hi, [&](unsigned a, unsigned b) {
+      const double ca = cen(a, bestAx), cb = cen(b, bestAx);
+      return ca < cb || (ca == cb && a < b);
+    });
+    return lo + bestK;
   };
   // bound of idx[lo, hi): C (float), R, RC (double)
   auto bound = [&](unsigned lo, unsigned hi, float C[3], double& R, double& RC) {
