@@ -305,9 +305,13 @@ __device__ __forceinline__ float canon_nan(float v) {
 // SIMD (S <= 6 with a small scene); measured +1-2 % over the unconstrained
 // 78-VGPR build at 6 waves/SIMD (C3, tile kernel).
 template <int S, int kVariant>
+#ifndef RTG_DEFAULT_MIN_WAVES  // compiler-setting A/B builds (tools/ab_build.sh) only
+#define RTG_DEFAULT_MIN_WAVES 7
+#endif
 struct MinWaves {
   static constexpr int value =
       (kVariant == 18 && S <= 6) ? 8
+      : (kVariant == 0 && S <= 6) ? RTG_DEFAULT_MIN_WAVES
       : ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
 };
 
@@ -611,17 +615,17 @@ void trace_samples_kernel(const KernelArgs a) {
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screen every sphere)
   // variant 21: kGroupsPerWave consecutive pixel groups per wave, in turn
+  // Compacted: the listed groups, dealt round-robin to the waves; otherwise K
+  // consecutive groups.  One loop, so trace_group is inlined once (the kernel
+  // body is ~50 KB of code per copy).
   constexpr int K = GroupsPerWave<kVariant>::value;
-  if (a.groupList) {  // compacted: the listed groups, dealt round-robin to the waves
-    const unsigned cnt = *(const RTG_CONST unsigned*)a.groupCount;
-    for (size_t idx = gw; idx < cnt; idx += a.nPersist)
-      trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
-                  (kVariant == 50)>(a, sc, ((const RTG_CONST unsigned*)a.groupList)[idx]);
-  } else {
-    for (int k = 0; k < K; ++k)
-      trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
-                  (kVariant == 50)>(a, sc, gw * K + k);
-  }
+  const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
+  size_t idx = list ? gw : gw * K;
+  const size_t end = list ? (size_t)*(const RTG_CONST unsigned*)a.groupCount : idx + K;
+  const size_t step = list ? (size_t)a.nPersist : 1;
+  for (; idx < end; idx += step)
+    trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
+                (kVariant == 50)>(a, sc, list ? (size_t)list[idx] : idx);
   record_wave(a, t0, gw);
 }
 
