@@ -537,7 +537,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
   if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 20 ||
-      variant == 21 || variant == 22 || variant == 50 || variant == 110)
+      variant == 21 || variant == 22 || variant == 23 || variant == 50 || variant == 110)
     ldsMats = false;
   TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr);
   if (!fn) {

@@ -154,6 +154,12 @@ struct Camera {
 // material {0,0,0, 0,0,0, opacity 0, n 1.0} (raytracer.h:694-697).
 struct Mat { V3 matte, gloss; float opacity, refr; };
 
+// Fused query forms (Scene::fuse bits; results identical, speed differs):
+// screen and exact root test in ONE wave-uniform loop over a sphere subset,
+// with scalar record loads, instead of a screen pass plus a per-lane
+// candidate loop with per-lane record gathers.
+enum : int { kFusePrim = 1, kFuseCone = 2, kFuseShadow = 4 };
+
 // Diagnostic probe slots (scenes without probes implement them as no-ops).
 // Operation counters (host simulation only; sc.count is a no-op on the GPU).
 enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, kCntEnterOK,
@@ -251,6 +257,39 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
     const float root = rtg_sqrtf(radicand);
     const float u0 = quot(-b + root, q);
     const float u1 = quot(-b - root, q);
+    if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+    if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
+  }
+  return sm;
+}
+
+// The same with the quotient path chosen for the whole wave (kFast: every
+// lane's denominator is in the Markstein range, all(q.fast)).
+template <bool kFast>
+RTG_HD float quot_k(float x, const RayQ& q) {
+  if constexpr (kFast) {
+    const float q0 = x * q.y;
+    const float r0 = fmaf(-q0, q.den, x);
+    const float q1 = fmaf(r0, q.y, q0);
+    const float r1 = fmaf(-q1, q.den, x);
+    return fmaf(r1, q.y, q1);
+  } else {
+    return quot(x, q);
+  }
+}
+
+template <bool kFast>
+RTG_HD float ray_sphere_k(const RayQ& q, V3 c, float r2, bool& res) {
+  V3 disp = vsub(q.o, c);
+  const float b = 2.0f * vdot(q.d, disp);
+  const float cc = vdot(disp, disp) - r2;
+  const float radicand = (b * b) - (q.a4 * cc);
+  float sm = 10000.f;
+  res = false;
+  if (radicand >= 0.0f) {
+    const float root = rtg_sqrtf(radicand);
+    const float u0 = quot_k<kFast>(-b + root, q);
+    const float u1 = quot_k<kFast>(-b - root, q);
     if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
     if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
   }
@@ -1125,9 +1164,40 @@ RTG_HD unsigned sign_mask(float v) {
 // increasing index order, one scalar load per sphere; pass 2 as blocked_mask.
 // Spheres outside `sel` cannot block (shadow_masks), so the answer equals
 // blocked_mask's, which equals the reference's hasClearLineOfSight.
+// Fused form (sc.fuse & kFuseShadow): one wave-uniform loop over `sel` in
+// index order; the lanes whose screen passes run the exact test right there
+// with the sphere's r^2 from a scalar load (no per-lane record gather, no
+// second loop), and the wave leaves once every lane is blocked.  Same answer:
+// blocked iff any sphere of `sel` blocks.
+template <bool kFast, class Scene>
+RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_t sel) {
+  bool blk = false;
+  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+    const unsigned i = (unsigned)__builtin_ctzll(m);
+    float rs;
+    const V3 c = sc.sphere_screen(i, rs);
+    const float r2 = sc.sphere_r2(i);
+    if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
+      sc.count(kCntShadowCand, 1);
+      bool res;
+      const float t = ray_sphere_k<kFast>(q, c, r2, res);
+      if (res && t < 1000.f) {
+        const V3 dist = vsmul(t, q.d);
+        if (vdot(dist, dist) < gap) blk = true;
+      }
+    }
+    if (sc.all(blk)) break;
+  }
+  return blk;
+}
+
 template <class Scene>
 RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
   const RayQ q = make_query(o, d);
+  if (sc.fuse & kFuseShadow) {
+    if (sc.all(q.fast)) return blocked_sel_fused<true>(sc, q, gap, sel);
+    return blocked_sel_fused<false>(sc, q, gap, sel);
+  }
   for (unsigned base = 0; base < 64u; base += 32u) {
     const unsigned u = (unsigned)(sel >> base);
     unsigned cand = 0;
@@ -1199,8 +1269,34 @@ RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, boo
 // that holds every sphere the ray can hit (cone_masks): pass 1 screens the
 // spheres of `sel` (one scalar load each), pass 2 tests the lane's candidates
 // in index order, so the answer is closest_hit_mask's.
+// Fused form (sc.fuse & kFuseCone): screen and exact test in one wave-uniform
+// loop in index order (strict <, so the first index still wins ties).
+template <bool kFast, class Scene>
+RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
+  float minT = 1000.f;
+  int best = -1;
+  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+    const unsigned i = (unsigned)__builtin_ctzll(m);
+    float rs;
+    const V3 c = sc.sphere_screen(i, rs);
+    const float r2 = sc.sphere_r2(i);
+    if (!(pass1_rad(q, c, rs) < 0.f)) {
+      sc.count(kCntFullCand, 1);
+      bool res;
+      const float t = ray_sphere_k<kFast>(q, c, r2, res);
+      if (res && t < minT) { minT = t; best = (int)i; }
+    }
+  }
+  tOut = minT;
+  return best;
+}
+
 template <class Scene>
 RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
+  if (sc.fuse & kFuseCone) {
+    if (sc.all(q.fast)) return closest_sel_fused<true>(sc, q, sel, tOut);
+    return closest_sel_fused<false>(sc, q, sel, tOut);
+  }
   uint64_t cand = 0;
   for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
@@ -1227,16 +1323,51 @@ RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut
 // Closest hit restricted to a wave-uniform subset `sel` of spheres 0..63
 // (bit i = sphere i may be hit; see primary_sphere_mask).  Spheres outside
 // `sel` cannot produce a valid root, so the result equals closest_hit_mask's.
+// Fused form (sc.fuse & kFusePrim): the roots straight from that radicand in
+// the same wave-uniform loop.  bp = 2 d.c is -b (negation is exact), so
+// -b + root = bp + root and -b - root = bp - root bit for bit (when b is a
+// zero, its sign changes neither sum nor the accept decision).
+template <bool kFast, class Scene>
+RTG_HD int closest_hit_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
+  float minT = 1000.f;
+  int best = -1;
+  const V3 d = q.d;
+  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+    const unsigned i = (unsigned)__builtin_ctzll(m);
+    float r2;
+    const V3 c = sc.sphere(i, r2);
+    const float bp = 2.0f * vdot(d, c);
+    const float rad = (bp * bp) - (q.a4 * sc.origin_c(i));
+    if (rad >= 0.0f) {
+      sc.count(kCntPrimCand, 1);
+      const float root = rtg_sqrtf(rad);
+      const float u0 = quot_k<kFast>(bp + root, q);
+      const float u1 = quot_k<kFast>(bp - root, q);
+      float sm = 10000.f;
+      bool res = false;
+      if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+      if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
+      if (res && sm < minT) { minT = sm; best = (int)i; }
+    }
+  }
+  tOut = minT;
+  return best;
+}
+
 template <class Scene>
 RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t sel) {
   const RayQ q = make_query(o, d);
-  float minT = 1000.f;
-  int best = -1;
-  uint64_t cand = 0;
   // The primary ray starts at the origin (main.cpp:417): disp = 0 - c = -c
   // exactly, so b = 2 d.disp = -(2 d.c) and b*b is (2 d.c)^2; the c term
   // |disp|^2 - r^2 is precomputed per sphere (origin_c).  Same radicand bits.
   (void)o;
+  if (sc.fuse & kFusePrim) {
+    if (sc.all(q.fast)) return closest_hit_sel_fused<true>(sc, q, sel, tOut);
+    return closest_hit_sel_fused<false>(sc, q, sel, tOut);
+  }
+  float minT = 1000.f;
+  int best = -1;
+  uint64_t cand = 0;
   for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform: scalar loop + scalar loads
     const unsigned i = (unsigned)__builtin_ctzll(m);
     float r2;
@@ -1353,37 +1484,6 @@ RTG_HD void candidate_masks64(const Scene& sc, V3 o, V3 d, float a4, unsigned& l
 #pragma unroll
     for (int q = 0; q < 4; ++q) { c[q] = cn[q]; r2[q] = rn[q]; }
   }
-}
-
-template <bool kFast>
-RTG_HD float quot_k(float x, const RayQ& q) {
-  if constexpr (kFast) {
-    const float q0 = x * q.y;
-    const float r0 = fmaf(-q0, q.den, x);
-    const float q1 = fmaf(r0, q.y, q0);
-    const float r1 = fmaf(-q1, q.den, x);
-    return fmaf(r1, q.y, q1);
-  } else {
-    return quot(x, q);
-  }
-}
-
-template <bool kFast>
-RTG_HD float ray_sphere_k(const RayQ& q, V3 c, float r2, bool& res) {
-  V3 disp = vsub(q.o, c);
-  const float b = 2.0f * vdot(q.d, disp);
-  const float cc = vdot(disp, disp) - r2;
-  const float radicand = (b * b) - (q.a4 * cc);
-  float sm = 10000.f;
-  res = false;
-  if (radicand >= 0.0f) {
-    const float root = rtg_sqrtf(radicand);
-    const float u0 = quot_k<kFast>(-b + root, q);
-    const float u1 = quot_k<kFast>(-b - root, q);
-    if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
-    if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
-  }
-  return sm;
 }
 
 // Pass 2 over the candidates of one 32-sphere half; kShadow: stop at the first

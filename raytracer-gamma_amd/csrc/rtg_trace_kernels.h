@@ -48,8 +48,11 @@ struct LdsFrames {
 
 // kBvh: the kernel instantiation for BVH scenes (n > 64); without it the BVH
 // branches compile away, so small scenes keep the smaller, faster kernel.
-template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = false>
+// kFuse: Scene::fuse bits (kFusePrim / kFuseCone / kFuseShadow, rtg_trace.h).
+template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = false,
+          int kFuse = 0>
 struct DevScene {
+  static constexpr int fuse = kFuse;
   FrameC* lfr;
   __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
   __device__ __forceinline__ bool any(bool b) const { return __ballot(b) != 0ull; }
@@ -95,6 +98,8 @@ struct DevScene {
     r2 = g[3];
     return v3(g[0], g[1], g[2]);
   }
+  // r^2 of sphere i (wave-uniform i: one scalar load)
+  __device__ __forceinline__ float sphere_r2(unsigned i) const { return geom[4 * i + 3]; }
   // Four consecutive sphere records: one 64-byte scalar load.
   __device__ __forceinline__ void sphere4(unsigned i, V3* c, float* r2) const {
     cfloat_p g = geom + 4 * i;
@@ -591,6 +596,13 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   }
 }
 
+// Fused query forms per variant (Scene::fuse bits, rtg_trace.h): every
+// sample-kernel variant except 23 (the two-pass queries, for A/B).
+template <int kVariant>
+struct FuseOf {
+  static constexpr int value = (kVariant == 23) ? 0 : (kFusePrim | kFuseCone | kFuseShadow);
+};
+
 template <int kVariant>
 struct GroupsPerWave {
   static constexpr int value = (kVariant == 21) ? 4 : 1;
@@ -608,7 +620,7 @@ __global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVaria
 void trace_samples_kernel(const KernelArgs a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh> sc;
+  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh, FuseOf<kVariant>::value> sc;
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
@@ -631,7 +643,8 @@ void trace_samples_kernel(const KernelArgs a) {
 
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
 //   0 (default) sample-parallel: one primary sample per lane, one-wave
-//     workgroups, scene tables read from global memory (trace_samples_kernel);
+//     workgroups, scene tables read from global memory (trace_samples_kernel),
+//     fused sphere queries (FuseOf);
 //     compacted launch for scenes of <= 64 spheres (cull_groups_kernel,
 //     rtg_kernel.hip); falls back to 9 when nAA > 8
 //   1 per-sample recursion, one sphere per step (first kernel)
@@ -653,6 +666,9 @@ void trace_samples_kernel(const KernelArgs a) {
 //   21 as 0 with four consecutive pixel groups per wave
 //   22 as 0 without the compacted launch (one wave per pixel group, every
 //      group traced: the default before cull_groups_kernel)
+//   23 as 0 with the two-pass queries (a screen loop, then a per-lane
+//      candidate loop with per-lane record gathers) for primary, cone-culled
+//      and shadow rays: the default before the fused queries (FuseOf)
 //   50 / 59: 0 / 9 with the OpenCL kernel's semantics (RTG_SEMANTICS_OPENCL;
 //     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
@@ -679,6 +695,7 @@ constexpr VariantInfo kVariants[] = {
     {14, kVariantSample, false}, {15, kVariantSample, false}, {16, kVariantSample, false},
     {17, kVariantSample, false}, {18, kVariantSample, false}, {19, kVariantSample, false},
     {20, kVariantSample, false}, {21, kVariantSample, false}, {22, kVariantSample, false},
+    {23, kVariantSample, false},
     {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
     {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
 };
@@ -693,7 +710,7 @@ static TraceFn trace_fn_v(bool lds) {
   if constexpr (V == 14 || V == 16 || V == 17)
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
   else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 20 || V == 21 || V == 22 ||
-                     V == 50 || V == 110)
+                     V == 23 || V == 50 || V == 110)
     return trace_samples_kernel<S, false, V>;
   else
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
@@ -726,6 +743,7 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh) {
     case 20: return trace_fn_v<S, 20>(lds);
     case 21: return trace_fn_v<S, 21>(lds);
     case 22: return trace_fn_v<S, 22>(lds);
+    case 23: return trace_fn_v<S, 23>(lds);
     case 50: return trace_fn_v<S, 50>(lds);
     case 59: return trace_fn_v<S, 59>(lds);
     case 104: return trace_fn_v<S, 104>(lds);

@@ -29,6 +29,7 @@ struct HostScene {
   unsigned n, m, n4;
   bool all(bool b) const { return b; }
   bool any(bool b) const { return b; }
+  int fuse = 0;  // fused query forms (rtg_trace.h kFuse*), set per variant
   const float* bvhNodes = nullptr;
   const float* bvhAux = nullptr;
   const int* bvhChild = nullptr;
@@ -64,6 +65,7 @@ struct HostScene {
     return rtg::v3(g[0], g[1], g[2]);
   }
   rtg::V3 sphere_lane(unsigned i, float& r2) const { return sphere(i, r2); }
+  float sphere_r2(unsigned i) const { return geom[4 * i + 3]; }
   void probe_begin(int) const {}
   struct Frames {
     rtg::FrameC* f;
@@ -132,14 +134,30 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
       case 0:
       case 14:
       case 15:
+      case 23:
       case 50: {  // sample-parallel kernel: samples traced one by one, summed in order
+        // primary-ray cull over the pixel's samples (the kernel's is per wave)
+        uint64_t sel = ~0ull;
+        const bool use = sc.n <= 64;
+        if (use) {
+          float x0, x1, y0, y1;
+          rtg::primary_bounds(cam, x, y, x0, x1, y0, y1);
+          const rtg::PrimBundle pb = rtg::primary_bundle(x0, x1, y0, y1, cam.zoom);
+          sel = 0;
+          for (unsigned k = 0; k < sc.n; ++k) {
+            float r2;
+            const rtg::V3 c = sc.sphere(k, r2);
+            const float* pk = sc.prim + 4 * k;
+            if (rtg::primary_possible(pb, c, pk[0], pk[1], pk[2])) sel |= 1ull << k;
+          }
+        }
         p = rtg::v3(0.f, 0.f, 0.f);
         for (int s = 0; s < cam.nAA * cam.nAA; ++s) {
           float rx, ry;
           const rtg::V3 d = rtg::sample_dir(cam, x, y, s / cam.nAA, s % cam.nAA, rx, ry);
           rtg::V3 c = g_variant == 15   ? rtg::trace_sample<S, 2>(sc, d, sc.frames())
-                      : g_variant == 50 ? rtg::trace_sample<S, 4, true>(sc, d, sc.frames())
-                                        : rtg::trace_sample<S, 4>(sc, d, sc.frames());
+                      : g_variant == 50 ? rtg::trace_sample<S, 4, true>(sc, d, sc.frames(), use, sel)
+                                        : rtg::trace_sample<S, 4>(sc, d, sc.frames(), use, sel);
           c = rtg::vsmul(cam.inv, c);
           p = rtg::vadd(p, c);
           g_counts[rtg::kCntSamples] += 1;
@@ -198,6 +216,10 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   sc.smask = ps.smask.empty() ? nullptr : ps.smask.data();
   sc.cone = ps.cone.empty() ? nullptr : ps.cone.data();
   sc.prim = ps.prim.data();
+  // the kernel's FuseOf (rtg_trace_kernels.h): sample-kernel variants but 23
+  sc.fuse = (g_variant == 0 || g_variant == 15 || g_variant == 50)
+                ? (rtg::kFusePrim | rtg::kFuseCone | rtg::kFuseShadow)
+                : 0;
   if (!ps.bvhChild.empty() && g_useBvh) {
     sc.bvhNodes = ps.bvhNodes.data();
     sc.bvhAux = ps.bvhAux.data();

@@ -132,8 +132,8 @@ def hostsim():
     return ctypes.CDLL(so)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 8, 9, 15],
-                ids=["v0", "v1", "v2", "v3", "v4", "v5", "v8", "v9", "v15"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 8, 9, 15, 23],
+                ids=["v0", "v1", "v2", "v3", "v4", "v5", "v8", "v9", "v15", "v23"])
 def variant(request, hostsim):
     hostsim.hostsim_set_variant(request.param)
     yield request.param

@@ -1,12 +1,22 @@
 #!/usr/bin/env bash
-# tools/ab_bench.sh LIB_A LIB_B [ROUNDS] [CONFIG] — interleaved same-box A/B of two
-# librtg.so builds on a bench config (kernel ms from HIP events per run).
+# tools/ab_bench.sh [-r ROUNDS] [-c CONFIG] LIB... — interleaved same-box A/B of
+# librtg.so builds on a bench config (kernel ms from HIP events per run, and
+# whether the frame's md5 matches the golden one).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-A=$1; B=$2; N=${3:-4}; C=${4:-c3}
-for r in $(seq $N); do
-  for L in "$A" "$B"; do
-    RTG_LIB=$L timeout -k 10 200 python bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline 2>/dev/null \
-      | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('$(basename $L)', d['kernel_ms'], d['parity'].get('fb_md5_match'))" || exit 1
+N=4
+C=c3
+while getopts "r:c:" o; do
+  case $o in
+    r) N=$OPTARG ;;
+    c) C=$OPTARG ;;
+    *) exit 2 ;;
+  esac
+done
+shift $((OPTIND - 1))
+for r in $(seq "$N"); do
+  for L in "$@"; do
+    RTG_LIB=$L timeout -k 10 200 python bench.py --config "$C" --steps 10 --warmup 2 --no-cpu-baseline 2>/dev/null \
+      | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('$C', '$(basename "$L")', d['kernel_ms'], d['parity'].get('fb_md5_match'), flush=True)" || exit 1
   done
 done
