@@ -158,7 +158,7 @@ struct Mat { V3 matte, gloss; float opacity, refr; };
 // screen and exact root test in ONE wave-uniform loop over a sphere subset,
 // with scalar record loads, instead of a screen pass plus a per-lane
 // candidate loop with per-lane record gathers.
-enum : int { kFusePrim = 1, kFuseCone = 2, kFuseShadow = 4 };
+enum : int { kFusePrim = 1, kFuseCone = 2, kFuseShadow = 4, kFuseEnter = 8 };
 
 // Diagnostic probe slots (scenes without probes implement them as no-ops).
 // Operation counters (host simulation only; sc.count is a no-op on the GPU).
@@ -379,16 +379,23 @@ constexpr float kContainDirMax = 3.0f;
 // union of the active lanes' overlap masks, shadow_masks in rtg_scene_pack.h):
 // every sphere outside `sel` provably fails the containment test for this
 // point, so the first containing sphere of `sel` in index order is the
-// reference's answer.  One scalar load of a containment record per sphere.
+// reference's answer.  One scalar load of a containment record per sphere,
+// and of the sphere's refractive index, returned in nT (the background's when
+// no sphere contains pt), so the caller needs no per-lane material gather.
 template <class Scene>
-RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel) {
+RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel, float& nT) {
   int found = -1;
+  nT = sc.refr((int)sc.n);  // background material (wave-uniform: scalar load)
   for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
     float cr;
     const V3 c = sc.sphere_contain(i, cr);
+    const float ni = sc.refr((int)i);  // scalar load, next to the record's
     const V3 dist = vsub(pt, c);
-    if (found < 0 && vdot(dist, dist) <= cr) found = (int)i;
+    if (found < 0 && vdot(dist, dist) <= cr) {
+      found = (int)i;
+      nT = ni;
+    }
     if (sc.all(found >= 0)) break;
   }
   return found;
@@ -516,18 +523,20 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 
   const V3 testPt = vadd(vsmul(0.01f, D), P);
   int tgt;
+  float nTgt;
   if (hit >= 0 && sc.has_smask()) {
     const bool ok = guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax;
     const uint64_t cu = sc.contain_union(hit, ok);
     sc.count(kCntContainMasked, 1);
     sc.count(kCntContainSel, __builtin_popcountll(cu));
-    tgt = primary_container_sel(sc, testPt, cu);
+    tgt = primary_container_sel(sc, testPt, cu, nTgt);
+    if (tgt < 0) tgt = (int)sc.n;  // background material
   } else {
     sc.count(kCntContainFull, 1);
     tgt = primary_container(sc, testPt);
+    if (tgt < 0) tgt = (int)sc.n;  // background material
+    nTgt = sc.refr(tgt);
   }
-  if (tgt < 0) tgt = (int)sc.n;  // background material
-  const float nTgt = sc.refr(tgt);
   const float ratio = nSrc / nTgt;
   const float sinA2 = ratio * sinA1;
 
@@ -1232,8 +1241,47 @@ RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
 // t_h, so the reference's closest hit (raytracer.h:145-194: strict <, index
 // order) is found among h and its overlap spheres, tested here in index order.
 // When !ok the caller runs the full query.
+// Fused form (sc.fuse & kFuseEnter), taken when every lane is `ok` (else it
+// returns at once and the caller runs the full query): one wave-uniform loop
+// over the union of the lanes' overlap masks, scalar record loads; a lane
+// tests sphere j only when j is in its own mask (`own`).  The winner is the
+// lexicographic minimum of (t, index) over h's root and the accepted roots
+// of the lane's mask spheres, which is what the index-order scan with strict
+// < keeps.
+template <class Scene>
+RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
+  float r2;
+  const V3 c = sc.sphere_lane((unsigned)h, r2);
+  bool res;
+  const float th = ray_sphere(q, c, r2, res);
+  const V3 e0 = vsub(q.o, c);
+  const V3 e1 = vsub(vadd(q.o, vsmul(th, q.d)), c);
+  const float g2 = sc.guard_r2((unsigned)h);
+  ok = res && th < 1000.f && vdot(e0, e0) <= g2 && vdot(e1, e1) <= g2;
+  tOut = 1000.f;
+  if (!sc.all(ok)) return -1;
+  uint64_t own;
+  const uint64_t u = sc.overlap_union(h, own);
+  own &= ~(1ull << h);
+  float minT = th;
+  int best = h;
+  for (uint64_t m = u; m; m &= m - 1) {  // wave-uniform
+    const unsigned j = (unsigned)__builtin_ctzll(m);
+    float rj2;
+    const V3 cj = sc.sphere(j, rj2);
+    if ((own >> j) & 1ull) {
+      bool rj;
+      const float t = ray_sphere(q, cj, rj2, rj);
+      if (rj && (t < minT || (t == minT && (int)j < best))) { minT = t; best = (int)j; }
+    }
+  }
+  tOut = minT;
+  return best;
+}
+
 template <class Scene>
 RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
+  if (sc.fuse & kFuseEnter) return closest_enter_fused(sc, q, h, tOut, ok);
   float r2;
   const V3 c = sc.sphere_lane((unsigned)h, r2);
   bool res;

@@ -178,6 +178,23 @@ struct DevScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   __device__ __forceinline__ float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
+  // Union of the active lanes' overlap masks (one scalar load per distinct
+  // h) and, in `own`, each lane's own mask.
+  __device__ __forceinline__ uint64_t overlap_union(int h, uint64_t& own) const {
+    uint64_t todo = __ballot(1);
+    uint64_t u = 0;
+    own = 0;
+    while (todo) {
+      const int src = __builtin_ctzll(todo);
+      const int h0 = __builtin_amdgcn_readlane(h, src);
+      const cuint_p w = smask + 2u * (m * n + (unsigned)h0);
+      const uint64_t mk = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      u |= mk;
+      if (h == h0) own = mk;
+      todo &= ~__ballot(h == h0);
+    }
+    return u;
+  }
   // Union of the active lanes' masks of table row `row` (wave-uniform): one
   // scalar mask load per distinct hit sphere among the lanes; every sphere if
   // a lane is not `ok` (its hit point failed the guard test).  Row l < m holds
@@ -600,7 +617,8 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
 // sample-kernel variant except 23 (the two-pass queries, for A/B).
 template <int kVariant>
 struct FuseOf {
-  static constexpr int value = (kVariant == 23) ? 0 : (kFusePrim | kFuseCone | kFuseShadow);
+  static constexpr int value =
+      (kVariant == 23) ? 0 : (kFusePrim | kFuseCone | kFuseShadow | kFuseEnter);
 };
 
 template <int kVariant>
@@ -667,8 +685,8 @@ void trace_samples_kernel(const KernelArgs a) {
 //   22 as 0 without the compacted launch (one wave per pixel group, every
 //      group traced: the default before cull_groups_kernel)
 //   23 as 0 with the two-pass queries (a screen loop, then a per-lane
-//      candidate loop with per-lane record gathers) for primary, cone-culled
-//      and shadow rays: the default before the fused queries (FuseOf)
+//      candidate loop with per-lane record gathers) for primary, cone-culled,
+//      shadow and entering rays: the default before the fused queries (FuseOf)
 //   50 / 59: 0 / 9 with the OpenCL kernel's semantics (RTG_SEMANTICS_OPENCL;
 //     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of

@@ -93,6 +93,10 @@ struct HostScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
+  uint64_t overlap_union(int h, uint64_t& own) const {
+    own = overlap_mask((unsigned)h);
+    return own;
+  }
   uint64_t shadow_union(unsigned l, int hit, bool guardOK) const {
     if (!guardOK) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
     const unsigned* w = smask + 2u * (l * n + (unsigned)hit);
@@ -218,7 +222,7 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   sc.prim = ps.prim.data();
   // the kernel's FuseOf (rtg_trace_kernels.h): sample-kernel variants but 23
   sc.fuse = (g_variant == 0 || g_variant == 15 || g_variant == 50)
-                ? (rtg::kFusePrim | rtg::kFuseCone | rtg::kFuseShadow)
+                ? (rtg::kFusePrim | rtg::kFuseCone | rtg::kFuseShadow | rtg::kFuseEnter)
                 : 0;
   if (!ps.bvhChild.empty() && g_useBvh) {
     sc.bvhNodes = ps.bvhNodes.data();
