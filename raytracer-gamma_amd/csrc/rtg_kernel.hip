@@ -106,9 +106,10 @@ __global__ __launch_bounds__(256) void ppm_kernel(const float* __restrict__ c, s
 // background matte is 0), and the pixel sum of +0 * inv is +0 in every
 // channel.  The other groups are appended to groupList (one atomic per wave)
 // for the trace kernel.  n <= 64 spheres.
-// Whether pixel group g can reach a sphere (the cull of trace_group).
-__device__ __forceinline__ bool group_live(const KernelArgs& a, size_t g, unsigned PPW,
-                                           size_t total) {
+// The spheres pixel group g can reach (the cull of trace_group): bit i set
+// when primary_possible keeps sphere i for the group's bundle.
+__device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, unsigned PPW,
+                                              size_t total) {
   const size_t p0 = g * PPW;
   const unsigned nv = (unsigned)((total - p0 < PPW) ? (total - p0) : PPW);
   unsigned col, lr;
@@ -137,21 +138,25 @@ __device__ __forceinline__ bool group_live(const KernelArgs& a, size_t g, unsign
   const PrimBundle pb = primary_bundle(x0, x1, y0, y1, a.cam.zoom);
   const RTG_CONST float* geom = (const RTG_CONST float*)a.geom;
   const RTG_CONST float* pc = (const RTG_CONST float*)a.prim;
-  bool possible = false;
+  uint64_t sel = 0;
   for (unsigned i = 0; i < a.n; ++i) {  // wave-uniform: scalar sphere records
     const RTG_CONST float* r = geom + 4 * i;
     const RTG_CONST float* k = pc + 4 * i;
-    possible |= primary_possible(pb, v3(r[0], r[1], r[2]), k[0], k[1], k[2]);
+    if (primary_possible(pb, v3(r[0], r[1], r[2]), k[0], k[1], k[2])) sel |= 1ull << i;
   }
-  return possible;
+  return sel;
 }
 
 // A block takes kCullGroups = 4 x 256 consecutive groups (one per lane per
 // round) and appends its live ones with ONE atomic: the atomics on the single
 // counter serialise in L2, so one per wave cost ~70 us on C3.
 constexpr unsigned kCullRounds = 4;
+// Each listed group's sphere mask goes to groupSel at the same list index:
+// the trace kernel takes it as the wave's primary-ray subset (one scalar
+// load) instead of recomputing the cull.
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
+                                                          unsigned long long* groupSel,
                                                           unsigned* groupCount) {
   __shared__ unsigned cnt[kCullRounds][4];
   __shared__ unsigned blockBase;
@@ -160,11 +165,12 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   const unsigned PPW = 64u / (nAA * nAA);
   const size_t total = (size_t)a.W * a.rowsLocal;
   const size_t blockG = (size_t)blockIdx.x * (256 * kCullRounds);
-  uint64_t live[kCullRounds];
+  uint64_t live[kCullRounds], sel[kCullRounds];
 #pragma unroll
   for (unsigned k = 0; k < kCullRounds; ++k) {
     const size_t g = blockG + k * 256 + threadIdx.x;
-    const bool possible = g < nGroups && group_live(a, g, PPW, total);
+    sel[k] = g < nGroups ? group_sel(a, g, PPW, total) : 0ull;
+    const bool possible = sel[k] != 0ull;
     // Zero-fill the pixels of all this wave's groups with coalesced stores
     // (the trace kernel, later on the same stream, overwrites the live ones).
     const size_t wg0 = g - lane;  // the wave's first group this round
@@ -191,17 +197,20 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     for (unsigned w = 0; w < 4; ++w)
       if (w < wave) off += cnt[k][w];
     const uint64_t m = live[k];
-    if ((m >> lane) & 1ull)
-      groupList[off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] =
-          (unsigned)(blockG + k * 256 + threadIdx.x);
+    if ((m >> lane) & 1ull) {
+      const unsigned at =
+          off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      groupList[at] = (unsigned)(blockG + k * 256 + threadIdx.x);
+      groupSel[at] = sel[k];
+    }
     for (unsigned w = wave; w < 4; ++w) off += cnt[k][w];
   }
 }
 
-static TraceFn pick_trace(int S, bool lds, int variant, bool bvh) {
+static TraceFn pick_trace(int S, bool lds, int variant, bool bvh, bool list) {
   switch (S) {
-#define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant, bvh);
+#define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant, bvh, list);
     RTG_CASE(1) RTG_CASE(2) RTG_CASE(3) RTG_CASE(4) RTG_CASE(5) RTG_CASE(6) RTG_CASE(7)
     RTG_CASE(8) RTG_CASE(9) RTG_CASE(10) RTG_CASE(11) RTG_CASE(12) RTG_CASE(13)
     RTG_CASE(14) RTG_CASE(15) RTG_CASE(16)
@@ -233,6 +242,7 @@ struct rtg_context {
   // the event recorded behind its last trace kernel.
   struct GroupSlot {
     unsigned* list = nullptr;  // listed pixel groups
+    unsigned long long* sel = nullptr;  // their primary-ray sphere masks
     unsigned* count = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;
@@ -368,6 +378,7 @@ int rtg_context_destroy(rtg_context* ctx) {
   (void)hipFree(ctx->timeline);
   for (auto& sl : ctx->slots) {
     (void)hipFree(sl.list);
+    (void)hipFree(sl.sel);
     (void)hipFree(sl.count);
     if (sl.done) (void)hipEventDestroy(sl.done);
   }
@@ -517,6 +528,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     return RTG_ERR_INVALID;
   }
   bool ldsMats = ctx->n + 1 <= kLdsMatMax;
+  if (stackSize < 1 || stackSize > RTG_MAX_STACK) {  // before anything is launched
+    rtg_set_error("no kernel for stackSize %d (valid: 1..%d)", stackSize, RTG_MAX_STACK);
+    return RTG_ERR_INVALID;
+  }
   KernelArgs a;
   int rc = make_camera(width, height, zoom, aliasFactor, &a.cam);
   if (rc) return rc;
@@ -537,14 +552,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
   if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 20 ||
-      variant == 21 || variant == 22 || variant == 23 || variant == 50 || variant == 110)
+      variant == 21 || variant == 22 || variant == 23 || variant == 24 || variant == 50 ||
+      variant == 110)
     ldsMats = false;
-  TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr);
-  if (!fn) {
-    rtg_set_error("no kernel for stackSize %d (valid: 1..%d), variant %d", stackSize,
-                  RTG_MAX_STACK, variant);
-    return RTG_ERR_INVALID;
-  }
   unsigned rows;
   if (rowList) {
     rows = nRowList;
@@ -589,6 +599,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.diag = nullptr;
   a.timeline = nullptr;
   a.groupList = nullptr;
+  a.groupSel = nullptr;
   a.groupCount = nullptr;
   a.nPersist = 0;
   if (variant >= 100) {
@@ -601,6 +612,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   unsigned threads = (unsigned)kBlock;
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
   rtg_context::GroupSlot* slot = nullptr;  // compacted launch scratch
+  bool listed = false;                     // compacted launch (kList kernel)
   if (sampleKernel) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
     const size_t groupsPerWave = variant == 21 ? 4 : 1;
@@ -620,6 +632,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     // one-wave workgroups traces the listed groups round-robin.
     const bool compact = tpb == 64 && variant != 21 && variant != 22;
     if (compact && ctx->n <= 64 && groups <= 0xFFFFFFFFull) {
+      listed = true;
       slot = &ctx->slots[ctx->nextSlot];
       ctx->nextSlot = (ctx->nextSlot + 1) % rtg_context::kSlots;
       if (!slot->done) HIP_TRY(hipEventCreateWithFlags(&slot->done, hipEventDisableTiming));
@@ -628,16 +641,20 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         // the slot's last kernel must be done before its list is freed
         HIP_TRY(hipEventSynchronize(slot->done));
         (void)hipFree(slot->list);
+        (void)hipFree(slot->sel);
         slot->list = nullptr;
+        slot->sel = nullptr;
         slot->cap = 0;
         HIP_TRY(hipMalloc(&slot->list, groups * sizeof(unsigned)));
+        HIP_TRY(hipMalloc(&slot->sel, groups * sizeof(unsigned long long)));
         slot->cap = groups;
       }
       if (!slot->count) HIP_TRY(hipMalloc(&slot->count, sizeof(unsigned)));
       HIP_TRY(hipMemsetAsync(slot->count, 0, sizeof(unsigned), (hipStream_t)stream));
       hipLaunchKernelGGL(cull_groups_kernel,
                          dim3((unsigned)((groups + 256 * kCullRounds - 1) / (256 * kCullRounds))),
-                         dim3(256), 0, (hipStream_t)stream, a, groups, slot->list, slot->count);
+                         dim3(256), 0, (hipStream_t)stream, a, groups, slot->list, slot->sel,
+                         slot->count);
       HIP_TRY(hipGetLastError());
       // about one wave per listed group: the benchmark scenes list 13-17 % of
       // their groups; a wave past the count exits at once, and a scene that
@@ -646,10 +663,17 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       if (persist < (size_t)ctx->numCU * 64) persist = (size_t)ctx->numCU * 64;
       if (ctx->persistPerCU > 0) persist = (size_t)ctx->numCU * ctx->persistPerCU;
       a.groupList = slot->list;
+      a.groupSel = slot->sel;
       a.groupCount = slot->count;
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
       grid = dim3(a.nPersist, 1);
     }
+  }
+  TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr, listed);
+  if (!fn) {
+    rtg_set_error("no kernel for stackSize %d (valid: 1..%d), variant %d", stackSize,
+                  RTG_MAX_STACK, variant);
+    return RTG_ERR_INVALID;
   }
   const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * threads * 16;
   const size_t lds = frameLds +

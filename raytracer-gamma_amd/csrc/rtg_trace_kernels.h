@@ -281,6 +281,7 @@ struct KernelArgs {
   // Compacted launch (cull_groups_kernel): the pixel groups some primary ray
   // may hit, their count, and the number of persistent waves; null otherwise.
   const unsigned* groupList;
+  const unsigned long long* groupSel;  // the listed groups' primary-ray sphere masks
   const unsigned* groupCount;
   unsigned nPersist;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
@@ -488,8 +489,11 @@ void trace_kernel(const KernelArgs a) {
 // Requires nAA^2 <= 64; the host launches the default kernel otherwise.
 // Pixel group gw (floor(64 / nAA^2) consecutive pixels of the shard's local
 // rows, all their samples) traced by one wave, entered converged.
+// hasSel: the cull pass already gave the group's primary-ray sphere subset
+// (gsel, compacted launch), so the wave skips its own cull.
 template <int S, int Q, bool kDiag, class Sc, bool kShfl = false, bool kCL = false>
-__device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw) {
+__device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw,
+                                            bool hasSel = false, uint64_t gsel = 0) {
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned SP = nAA * nAA;
@@ -520,7 +524,10 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
   // Primary-ray cull over the wave's sample directions (wave converged).
   uint64_t primSel = ~0ull;
   bool usePrim = false;
-  if (RTG_PROBE_FLOOR < 2 && a.n <= 64) {
+  if (hasSel) {
+    primSel = gsel;
+    usePrim = true;
+  } else if (RTG_PROBE_FLOOR < 2 && a.n <= 64) {
     float x0, x1, y0, y1;
     // Wave-uniform: do the wave's valid pixels lie in one row?  Then the
     // bounds are four lanes' values, since every float step of main.cpp:
@@ -632,8 +639,11 @@ struct SampleThreads {
 };
 
 // One launch, one pixel group per wave: one-wave workgroups (default), or
-// four-wave ones (variant 14).
-template <int S, bool kLds, int kVariant, bool kBvh = false>
+// four-wave ones (variant 14).  kList: the compacted launch (the launcher
+// guarantees a.groupList): the listed groups, dealt round-robin to the waves,
+// with the cull pass's sphere masks; otherwise K consecutive groups per wave.
+// Separate instantiations keep each loop's registers to itself.
+template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false>
 __global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
 void trace_samples_kernel(const KernelArgs a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
@@ -643,19 +653,24 @@ void trace_samples_kernel(const KernelArgs a) {
   stage_scene<S, kLds, kThreads>(a, sc);
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
   const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  // variant 15: the previous default (shadow rays screen every sphere)
+  // variant 15: the previous default (shadow rays screening every sphere)
   // variant 21: kGroupsPerWave consecutive pixel groups per wave, in turn
-  // Compacted: the listed groups, dealt round-robin to the waves; otherwise K
-  // consecutive groups.  One loop, so trace_group is inlined once (the kernel
-  // body is ~50 KB of code per copy).
-  constexpr int K = GroupsPerWave<kVariant>::value;
-  const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
-  size_t idx = list ? gw : gw * K;
-  const size_t end = list ? (size_t)*(const RTG_CONST unsigned*)a.groupCount : idx + K;
-  const size_t step = list ? (size_t)a.nPersist : 1;
-  for (; idx < end; idx += step)
-    trace_group<S, (kVariant == 15 ? 2 : 4), (kVariant >= 100), decltype(sc), (kVariant == 19),
-                (kVariant == 50)>(a, sc, list ? (size_t)list[idx] : idx);
+  constexpr int Q = (kVariant == 15) ? 2 : 4;
+  constexpr bool kDiag = kVariant >= 100;
+  if constexpr (kList) {
+    const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
+    // variant 24: the wave recomputes its primary cull (no cull-pass masks)
+    const RTG_CONST unsigned long long* gsel = (const RTG_CONST unsigned long long*)a.groupSel;
+    const size_t cnt = *(const RTG_CONST unsigned*)a.groupCount;
+    for (size_t idx = gw; idx < cnt; idx += a.nPersist)
+      trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(
+          a, sc, list[idx], kVariant != 24, kVariant != 24 ? (uint64_t)gsel[idx] : 0ull);
+  } else {
+    constexpr int K = GroupsPerWave<kVariant>::value;
+    for (int k = 0; k < K; ++k)
+      trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(a, sc,
+                                                                                 gw * K + k);
+  }
   record_wave(a, t0, gw);
 }
 
@@ -687,6 +702,8 @@ void trace_samples_kernel(const KernelArgs a) {
 //   23 as 0 with the two-pass queries (a screen loop, then a per-lane
 //      candidate loop with per-lane record gathers) for primary, cone-culled,
 //      shadow and entering rays: the default before the fused queries (FuseOf)
+//   24 as 0 with each wave computing its primary-ray cull instead of taking
+//      the cull pass's per-group sphere mask
 //   50 / 59: 0 / 9 with the OpenCL kernel's semantics (RTG_SEMANTICS_OPENCL;
 //     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
@@ -713,7 +730,7 @@ constexpr VariantInfo kVariants[] = {
     {14, kVariantSample, false}, {15, kVariantSample, false}, {16, kVariantSample, false},
     {17, kVariantSample, false}, {18, kVariantSample, false}, {19, kVariantSample, false},
     {20, kVariantSample, false}, {21, kVariantSample, false}, {22, kVariantSample, false},
-    {23, kVariantSample, false},
+    {23, kVariantSample, false}, {24, kVariantSample, false},
     {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
     {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
 };
@@ -723,15 +740,32 @@ inline const VariantInfo* variant_info(int v) {
   return nullptr;
 }
 
+// list: the compacted launch (kList instantiations exist for the one-wave
+// sample kernels that the launcher compacts, CompactVariant).
+// (launch_trace compacts every one-wave sample kernel but 21 and 22); a list
+// request for any other variant gets nullptr, an error, never a wrong frame.
+template <int V>
+struct CompactVariant {
+  static constexpr bool value = V == 0 || V == 15 || V == 17 || V == 18 || V == 19 || V == 20 ||
+                                V == 23 || V == 24 || V == 50 || V == 110;
+};
 template <int S, int V>
-static TraceFn trace_fn_v(bool lds) {
-  if constexpr (V == 14 || V == 16 || V == 17)
+static TraceFn trace_fn_v(bool lds, bool list) {
+  if (list && !CompactVariant<V>::value) return nullptr;
+  if constexpr (V == 17) {
+    if (list)
+      return lds ? trace_samples_kernel<S, true, V, false, true>
+                 : trace_samples_kernel<S, false, V, false, true>;
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  else if constexpr (V == 0 || V == 15 || V == 18 || V == 19 || V == 20 || V == 21 || V == 22 ||
-                     V == 23 || V == 50 || V == 110)
+  } else if constexpr (V == 14 || V == 16) {
+    return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
+  } else if constexpr (CompactVariant<V>::value) {
+    return list ? trace_samples_kernel<S, false, V, false, true> : trace_samples_kernel<S, false, V>;
+  } else if constexpr (V == 21 || V == 22) {
     return trace_samples_kernel<S, false, V>;
-  else
+  } else {
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
+  }
 }
 // BVH scenes: the default kernels (and their diagnostic and OpenCL-semantics
 // forms) have kBvh instantiations; other A/B variants run BVH scenes through
@@ -749,42 +783,44 @@ static TraceFn trace_fn_bvh(bool lds, int variant) {
   }
 }
 template <int S>
-static TraceFn trace_fn(bool lds, int variant, bool bvh) {
+static TraceFn trace_fn(bool lds, int variant, bool bvh, bool list) {
   if (bvh) {
+    if (list) return nullptr;  // BVH scenes (n > 64) are never compacted
     if (TraceFn f = trace_fn_bvh<S>(lds, variant)) return f;
   }
   switch (variant) {
-    case 100: return trace_fn_v<S, 100>(lds);
-    case 110: return trace_fn_v<S, 110>(lds);
-    case 18: return trace_fn_v<S, 18>(lds);
-    case 19: return trace_fn_v<S, 19>(lds);
-    case 20: return trace_fn_v<S, 20>(lds);
-    case 21: return trace_fn_v<S, 21>(lds);
-    case 22: return trace_fn_v<S, 22>(lds);
-    case 23: return trace_fn_v<S, 23>(lds);
-    case 50: return trace_fn_v<S, 50>(lds);
-    case 59: return trace_fn_v<S, 59>(lds);
-    case 104: return trace_fn_v<S, 104>(lds);
-    case 1: return trace_fn_v<S, 1>(lds);
-    case 4: return trace_fn_v<S, 4>(lds);
-    case 5: return trace_fn_v<S, 5>(lds);
-    case 6: return trace_fn_v<S, 6>(lds);
-    case 8: return trace_fn_v<S, 8>(lds);
-    case 9: return trace_fn_v<S, 9>(lds);
-    case 14: return trace_fn_v<S, 14>(lds);
-    case 15: return trace_fn_v<S, 15>(lds);
-    case 16: return trace_fn_v<S, 16>(lds);
-    case 17: return trace_fn_v<S, 17>(lds);
-    case 108: return trace_fn_v<S, 108>(lds);
-    case 2: return trace_fn_v<S, 2>(lds);
-    case 3: return trace_fn_v<S, 3>(lds);
-    case 0: return trace_fn_v<S, 0>(lds);
+    case 100: return trace_fn_v<S, 100>(lds, list);
+    case 110: return trace_fn_v<S, 110>(lds, list);
+    case 18: return trace_fn_v<S, 18>(lds, list);
+    case 19: return trace_fn_v<S, 19>(lds, list);
+    case 20: return trace_fn_v<S, 20>(lds, list);
+    case 21: return trace_fn_v<S, 21>(lds, list);
+    case 22: return trace_fn_v<S, 22>(lds, list);
+    case 23: return trace_fn_v<S, 23>(lds, list);
+    case 24: return trace_fn_v<S, 24>(lds, list);
+    case 50: return trace_fn_v<S, 50>(lds, list);
+    case 59: return trace_fn_v<S, 59>(lds, list);
+    case 104: return trace_fn_v<S, 104>(lds, list);
+    case 1: return trace_fn_v<S, 1>(lds, list);
+    case 4: return trace_fn_v<S, 4>(lds, list);
+    case 5: return trace_fn_v<S, 5>(lds, list);
+    case 6: return trace_fn_v<S, 6>(lds, list);
+    case 8: return trace_fn_v<S, 8>(lds, list);
+    case 9: return trace_fn_v<S, 9>(lds, list);
+    case 14: return trace_fn_v<S, 14>(lds, list);
+    case 15: return trace_fn_v<S, 15>(lds, list);
+    case 16: return trace_fn_v<S, 16>(lds, list);
+    case 17: return trace_fn_v<S, 17>(lds, list);
+    case 108: return trace_fn_v<S, 108>(lds, list);
+    case 2: return trace_fn_v<S, 2>(lds, list);
+    case 3: return trace_fn_v<S, 3>(lds, list);
+    case 0: return trace_fn_v<S, 0>(lds, list);
     default: return nullptr;  // not in kVariants
   }
 }
 
 // One per stack size, defined in rtg_trace_s<S>.hip.
-#define RTG_DECL(k) TraceFn trace_fn_s##k(bool lds, int variant, bool bvh);
+#define RTG_DECL(k) TraceFn trace_fn_s##k(bool lds, int variant, bool bvh, bool list);
 RTG_DECL(1) RTG_DECL(2) RTG_DECL(3) RTG_DECL(4) RTG_DECL(5) RTG_DECL(6) RTG_DECL(7)
 RTG_DECL(8) RTG_DECL(9) RTG_DECL(10) RTG_DECL(11) RTG_DECL(12) RTG_DECL(13)
 RTG_DECL(14) RTG_DECL(15) RTG_DECL(16)

@@ -106,7 +106,7 @@ def test_random_scenes_vs_oracle(R, oracle):
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
 
 
-@pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23])
+@pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23, 24])
 def test_random_scenes_vs_oracle_variants(R, oracle, torch_cuda, variant):
     """Mapping variants over random scenes, sizes and alias factors (the
     sample-parallel kernel packs 64 // nAA^2 pixels per wave and falls back to
@@ -181,7 +181,7 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
     ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23])
+@pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23, 24])
 def test_variant_full_frames(R, golden, torch_cuda, variant):
     """Kernel mappings over whole frames, sharded frames, row lists and
     back-to-back launches on two streams."""
@@ -261,7 +261,7 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 100, 108, 110])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 100, 108, 110])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda

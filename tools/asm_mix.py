@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""tools/asm_mix.py ASM [VARIANT] [BVH] — static instruction mix of one
+"""tools/asm_mix.py ASM [VARIANT] [BVH] [LIST] — static instruction mix of one
 trace_samples_kernel instantiation in a `make asm` listing (build/rtg_trace_sS.s):
 instruction classes, f64 opcodes, scratch accesses and the register/occupancy
 summary the compiler prints after the function."""
@@ -18,9 +18,11 @@ def main():
     path = sys.argv[1]
     variant = sys.argv[2] if len(sys.argv) > 2 else "0"
     bvh = sys.argv[3] if len(sys.argv) > 3 else "0"
+    lst = sys.argv[4] if len(sys.argv) > 4 else "1"  # kList: the compacted launch
     text = open(path).read()
     s = re.search(r"_ZN3rtg20trace_samples_kernelILi(\d+)E", text).group(1)
-    sym = "_ZN3rtg20trace_samples_kernelILi%sELb0ELi%sELb%sEEEvNS_10KernelArgsE" % (s, variant, bvh)
+    sym = "_ZN3rtg20trace_samples_kernelILi%sELb0ELi%sELb%sELb%sEEEvNS_10KernelArgsE" % (
+        s, variant, bvh, lst)
     body, tail = kernel_body(text, sym)
     ops = [l.split()[0] for l in body.split("\n")
            if l.startswith("\t") and l.strip() and not l.strip().startswith((".", ";"))]
