@@ -165,7 +165,8 @@ enum : int { kFusePrim = 1, kFuseCone = 2, kFuseShadow = 4, kFuseEnter = 8 };
 enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, kCntEnterOK,
              kCntFullQ, kCntFullCand, kCntShadowQ, kCntShadowSel, kCntShadowCand,
              kCntContainMasked, kCntContainSel, kCntContainFull, kCntRefraction, kCntReflPush,
-             kCntBvhNodeTests, kCntBvhSphereTests, kCntConeQ, kCntConeSel, kCntSlots };
+             kCntBvhNodeTests, kCntBvhSphereTests, kCntConeQ, kCntConeSel,
+             kCntBvhShadowQ, kCntBvhShadowNodeTests, kCntBvhShadowSphereTests, kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
@@ -482,6 +483,56 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
   return sum;
 }
 
+// The f64 islands' square root and quotient without the general
+// sequences' scaling and special-case fix-ups, for the operands where those
+// are the identity: the same operations as the compiler's IEEE expansions
+// (v_rsq_f64 / v_rcp_f64 refined by fused Newton steps), so the same
+// correctly rounded results.  tests/fpcheck/fpcheck_gpu.hip checks both
+// against sqrt() and a / b bit for bit on the GPU (every sinA1 operand, and
+// 2^32 random Fresnel operand pairs).
+//  * sqrt_d_unit(y), y = 1 - (double)(c * c) for a float c in (-1, 1)
+//    (calculateRefraction, raytracer.h:683): y is 0 or in [2^-24, 1] (or NaN,
+//    which stays NaN); 0 is the one operand the refinement cannot take.
+//  * div_d_fresnel(a, b, fast), a = num^2 and b = den^2 >= 1e-6 the exact
+//    squares of polarisedReflection's float sums (raytracer.h:388-393):
+//    `fast` (the caller's float check |l|, |r| <= 2^100) keeps both in
+//    (2^-20, 2^202], where the general sequence scales nothing.
+RTG_HD double sqrt_d_unit(double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double g = __builtin_amdgcn_rsq(y);
+  double s = y * g;
+  double h = g * 0.5;
+  const double r = fma(-h, s, 0.5);
+  s = fma(s, r, s);
+  h = fma(h, r, h);
+  double d = fma(-s, s, y);
+  s = fma(d, h, s);
+  d = fma(-s, s, y);
+  s = fma(d, h, s);
+  return y == 0.0 ? 0.0 : s;
+#else
+  return sqrt(y);
+#endif
+}
+RTG_HD double div_d_fresnel(double a, double b, bool fast) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (fast) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    const double q = a * y;
+    const double r = fma(-b, q, a);
+    return fma(r, y, q);
+  }
+  no_speculate();
+#else
+  (void)fast;
+#endif
+  return a / b;
+}
+
 // raytracer.h:370-403 (f64 island).  kCL: the OpenCL kernel's all-float
 // version, raytrace_kernel.cl:399-432.
 template <bool kCL = false>
@@ -501,7 +552,8 @@ RTG_HD float polarised_reflection(float n1, float n2, float cosA1, float cosA2) 
   double den = (double)(left + right);
   den *= den;
   if (den < (double)1.0e-6f) return 1.f;
-  float refl = (float)((num * num) / den);
+  const bool fast = fabsf(left) <= 0x1p100f && fabsf(right) <= 0x1p100f;
+  float refl = (float)div_d_fresnel(num * num, den, fast);
   if (refl > 1.f) refl = 1.f;
   return refl;
 }
@@ -519,7 +571,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   if (cosA1 <= -1.0f) { cosA1 = -1.f; sinA1 = 0.f; }
   else if (cosA1 >= 1.f) { cosA1 = 1.f; sinA1 = 0.f; }
   else if (kCL) { sinA1 = rtg_sqrtf(1.f - (cosA1 * cosA1)); }  // raytrace_kernel.cl:507
-  else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }
+  else { sinA1 = (float)sqrt_d_unit(1.0 - (double)(cosA1 * cosA1)); }
 
   const V3 testPt = vadd(vsmul(0.01f, D), P);
   int tgt;
@@ -576,7 +628,9 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   if (cosA1 < 0.f) cosA2 = -cosA2;
   const float Rs = polarised_reflection<kCL>(nSrc, nTgt, cosA1, cosA2);
   const float Rp = polarised_reflection<kCL>(nSrc, nTgt, cosA2, cosA1);
-  R = (float)((double)(Rs + Rp) * 0.5);
+  // (float)((double)(Rs + Rp) * 0.5) (raytracer.h:801): the f64 product is
+  // exact, so its rounding to float is the float product's.
+  R = (Rs + Rp) * 0.5f;
   return tgt;
 }
 
@@ -980,7 +1034,7 @@ RTG_HD void push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2
 // the prune.  `active`: the lane still queries; `reach`: its pruning reach.
 template <class Scene, class Leaf>
 RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active, float reach,
-                         BvhStack& st, Leaf&& leaf) {
+                         BvhStack& st, Leaf&& leaf, bool shadowQ = false) {
   V3 c[4];
   float w[4], rp[4], cr[4];
   int ch[4];
@@ -999,14 +1053,14 @@ RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool activ
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
     const bool near = !beyond(p2, rp[k], reach);
     if (x > 0) {
-      sc.count(kCntBvhNodeTests, 1);
+      sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
       const float v = fmaf(xd, xd, fmaf(-q.apB, p2 - w[k], 0x1p-100f));  // pass1_bound
       if (sc.any(active && near && !(v < 0.f))) {
         pc[k] = x;
         pk[k] = sc.first_lane(p2);
       }
     } else {
-      sc.count(kCntBvhSphereTests, 1);
+      sc.count(shadowQ ? kCntBvhShadowSphereTests : kCntBvhSphereTests, 1);
       const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - w[k], 0x1p-100f));  // pass1_rad
       if (active && near && !(v < 0.f)) leaf((unsigned)~x);
     }
@@ -1043,6 +1097,7 @@ template <class Scene>
 RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   bool blk = false;
   const float reach = norm_up(gap);
+  sc.count(kCntBvhShadowQ, 1);
   BvhStack st(sc.bvh_stack());
   st.push(0);
   while (!st.empty()) {  // wave-uniform
@@ -1058,7 +1113,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
       }
-    });
+    }, true);
   }
   return blk;
 }

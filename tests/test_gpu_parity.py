@@ -496,3 +496,20 @@ def test_fast_sqrt_rcp_exhaustive():
     assert rcp_in == 0x7E000000 - 0x01000000 + 1
     assert (sqrt_lib, sqrt_exact, sqrt_all) == (0, 0, 0), list(out)
     assert (rcp_lib, rcp_exact, rcp_all) == (0, 0, 0), list(out)
+
+
+def test_fast_f64_islands():
+    """rtg_trace.h's trimmed f64 square root and quotient of the refraction
+    (sqrt_d_unit for sinA1 = sqrt(1 - cos^2), raytracer.h:683, and
+    div_d_fresnel for polarisedReflection's quotient, raytracer.h:388-393)
+    against sqrt() and the IEEE division bit for bit on the GPU: every float
+    cosine in [0, 1) and 2^32 random Fresnel operand pairs
+    (tests/fpcheck/fpcheck_gpu.hip)."""
+    so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fpcheck", "libfpcheck_gpu.so")
+    L = ctypes.CDLL(so)
+    out = (ctypes.c_ulonglong * 4)()
+    assert L.fpcheck_f64_run(ctypes.c_ulonglong(0), out) == 0
+    sqrt_in, sqrt_bad, div_in, div_bad = list(out)
+    assert sqrt_in == 0x3F800000
+    assert div_in > 3 * 10**9, list(out)
+    assert (sqrt_bad, div_bad) == (0, 0), list(out)

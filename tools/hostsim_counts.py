@@ -16,7 +16,8 @@ from conftest import BUILD, GOLDEN, P, load_scene  # noqa: E402
 
 NAMES = ["samples", "primQ", "primSel", "primCand", "enterQ", "enterOK", "fullQ", "fullCand",
          "shadowQ", "shadowSel", "shadowCand", "containMasked", "containSel", "containFull",
-         "refraction", "reflPush", "bvhNodeTests", "bvhSphereTests", "coneQ", "coneSel"]
+         "refraction", "reflPush", "bvhNodeTests", "bvhSphereTests", "coneQ", "coneSel",
+         "bvhShadowQ", "bvhShadowNodeTests", "bvhShadowSphereTests"]
 
 
 def main():
@@ -28,7 +29,7 @@ def main():
     W, H, S = c["W"], c["H"], c["stack_size"]
     rows = np.arange(0, H, stride, dtype=np.uint32)
     out = np.zeros((len(rows), W, 3), np.float32)
-    cnt = (ctypes.c_long * 20)()
+    cnt = (ctypes.c_long * len(NAMES))()
     hs.hostsim_set_variant(0)
     hs.hostsim_counts(cnt, 1)
     rc = hs.hostsim_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
