@@ -652,7 +652,10 @@ void trace_samples_kernel(const KernelArgs a) {
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
-  const size_t gw = (size_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  // the wave's index, wave-uniform (readfirstlane: an SGPR, so the list and
+  // mask reads below are scalar loads and the group set-up is scalar work)
+  const size_t gw = (size_t)blockIdx.x * (kThreads / 64) +
+                    (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // variant 15: the previous default (shadow rays screening every sphere)
   // variant 21: kGroupsPerWave consecutive pixel groups per wave, in turn
   constexpr int Q = (kVariant == 15) ? 2 : 4;
@@ -661,10 +664,12 @@ void trace_samples_kernel(const KernelArgs a) {
     const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
     // variant 24: the wave recomputes its primary cull (no cull-pass masks)
     const RTG_CONST unsigned long long* gsel = (const RTG_CONST unsigned long long*)a.groupSel;
-    const size_t cnt = *(const RTG_CONST unsigned*)a.groupCount;
-    for (size_t idx = gw; idx < cnt; idx += a.nPersist)
+    const unsigned cnt = *(const RTG_CONST unsigned*)a.groupCount;
+    for (unsigned idx = (unsigned)gw; idx < cnt; idx += a.nPersist) {
+      const unsigned g = __builtin_amdgcn_readfirstlane(list[idx]);
       trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(
-          a, sc, list[idx], kVariant != 24, kVariant != 24 ? (uint64_t)gsel[idx] : 0ull);
+          a, sc, g, kVariant != 24, kVariant != 24 ? (uint64_t)gsel[idx] : 0ull);
+    }
   } else {
     constexpr int K = GroupsPerWave<kVariant>::value;
     for (int k = 0; k < K; ++k)
