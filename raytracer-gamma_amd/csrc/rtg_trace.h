@@ -170,6 +170,15 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
+// Finer regions, recorded only by RTG_DIAG_SPLIT builds (in slots 1, 4, 5, 6
+// instead of shadow, matte, push, unwind): the shading set-up after the
+// closest-hit query (hit record, P, N, material, guard test), the refraction
+// target's containment search, the Fresnel factor, and sinA1.
+#ifndef RTG_DIAG_SPLIT
+#define RTG_DIAG_SPLIT 0
+#endif
+enum : int { kProbeSplitBase = 100, kProbeSplitSetup = 101, kProbeSplitContain = 104,
+             kProbeSplitFresnel = 105, kProbeSplitSin = 106 };
 
 // Split frame used by trace_sample: the part every unwind step touches
 // (colour, stage flags, refractive material) is 16 bytes and can live in LDS;
@@ -571,8 +580,13 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   if (cosA1 <= -1.0f) { cosA1 = -1.f; sinA1 = 0.f; }
   else if (cosA1 >= 1.f) { cosA1 = 1.f; sinA1 = 0.f; }
   else if (kCL) { sinA1 = rtg_sqrtf(1.f - (cosA1 * cosA1)); }  // raytrace_kernel.cl:507
-  else { sinA1 = (float)sqrt_d_unit(1.0 - (double)(cosA1 * cosA1)); }
+  else {
+    sc.probe_begin(kProbeSplitSin);
+    sinA1 = (float)sqrt_d_unit(1.0 - (double)(cosA1 * cosA1));
+    sc.probe_end(kProbeSplitSin);
+  }
 
+  sc.probe_begin(kProbeSplitContain);
   const V3 testPt = vadd(vsmul(0.01f, D), P);
   int tgt;
   float nTgt;
@@ -589,6 +603,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
     if (tgt < 0) tgt = (int)sc.n;  // background material
     nTgt = sc.refr(tgt);
   }
+  sc.probe_end(kProbeSplitContain);
   const float ratio = nSrc / nTgt;
   const float sinA2 = ratio * sinA1;
 
@@ -624,6 +639,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
     }
     dirOut = dir;
   }
+  sc.probe_begin(kProbeSplitFresnel);
   float cosA2 = rtg_sqrtf(1.f - (sinA2 * sinA2));
   if (cosA1 < 0.f) cosA2 = -cosA2;
   const float Rs = polarised_reflection<kCL>(nSrc, nTgt, cosA1, cosA2);
@@ -631,6 +647,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   // (float)((double)(Rs + Rp) * 0.5) (raytracer.h:801): the f64 product is
   // exact, so its rounding to float is the float product's.
   R = (Rs + Rp) * 0.5f;
+  sc.probe_end(kProbeSplitFresnel);
   return tgt;
 }
 
@@ -695,6 +712,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     if (hit < 0) {
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
+      sc.probe_begin(kProbeSplitSetup);
       float r2unused;
       const V3 c = sc.sphere((unsigned)hit, r2unused);
       const V3 P = vadd(o, vsmul(t, d));
@@ -708,6 +726,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         const V3 e = vsub(P, c);
         guardOK = vdot(e, e) <= sc.guard_r2((unsigned)hit);
       }
+      sc.probe_end(kProbeSplitSetup);
       if (op > 0.f) {
         V3 tmp = vmul(I, mh.matte);
         tmp = vsmul(op, tmp);

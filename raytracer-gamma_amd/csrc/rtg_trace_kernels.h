@@ -63,14 +63,28 @@ struct DevScene {
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
   mutable unsigned long long acc[kProbeSlots];
   mutable unsigned long long t0[kProbeSlots];
-  __device__ __forceinline__ void probe_begin(int slot) const {
+  // RTG_DIAG_SPLIT builds (diagnostic A/B libraries only) re-assign slots 1
+  // and 4-6 to the finer regions kProbeSplit* (rtg_trace.h).
+  __device__ __forceinline__ static int probe_slot(int slot) {
+    if (RTG_DIAG_SPLIT) {
+      if (slot >= kProbeSplitBase) return slot - kProbeSplitBase;
+      if (slot == kProbeShadow || (slot >= kProbeMatte && slot <= kProbeUnwind)) return -1;
+      return slot;
+    }
+    return slot >= kProbeSplitBase ? -1 : slot;
+  }
+  __device__ __forceinline__ void probe_begin(int slot0) const {
+    const int slot = probe_slot(slot0);
+    if (slot < 0) return;
     if constexpr (kDiag) {
       __builtin_amdgcn_sched_barrier(0);
       t0[slot] = __builtin_amdgcn_s_memtime();
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  __device__ __forceinline__ void probe_end(int slot) const {
+  __device__ __forceinline__ void probe_end(int slot0) const {
+    const int slot = probe_slot(slot0);
+    if (slot < 0) return;
     if constexpr (kDiag) {
       __builtin_amdgcn_sched_barrier(0);
       acc[slot] += __builtin_amdgcn_s_memtime() - t0[slot];
