@@ -713,18 +713,19 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
       sc.probe_begin(kProbeSplitSetup);
-      float r2unused;
-      const V3 c = sc.sphere((unsigned)hit, r2unused);
+      V3 c;
+      float g2;
+      Mat mh;
+      sc.hit_data(hit, c, g2, mh);  // centre, guard radius^2, material of the hit sphere
       const V3 P = vadd(o, vsmul(t, d));
       const V3 N = vnorm(vsub(P, c));
-      const Mat mh = sc.mat(hit);
       const float op = mh.opacity;
       const float tr = 1.f - op;
       V3 colour = v3(0.f, 0.f, 0.f);
       bool guardOK = false;
       if constexpr (Q == 4) {  // P in the hit sphere's guard ball (shadow/overlap masks)
         const V3 e = vsub(P, c);
-        guardOK = vdot(e, e) <= sc.guard_r2((unsigned)hit);
+        guardOK = vdot(e, e) <= g2;
       }
       sc.probe_end(kProbeSplitSetup);
       if (op > 0.f) {
@@ -1324,13 +1325,12 @@ RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
 // < keeps.
 template <class Scene>
 RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
-  float r2;
-  const V3 c = sc.sphere_lane((unsigned)h, r2);
+  float r2, g2;
+  const V3 c = sc.sphere_guard(h, r2, g2);
   bool res;
   const float th = ray_sphere(q, c, r2, res);
   const V3 e0 = vsub(q.o, c);
   const V3 e1 = vsub(vadd(q.o, vsmul(th, q.d)), c);
-  const float g2 = sc.guard_r2((unsigned)h);
   ok = res && th < 1000.f && vdot(e0, e0) <= g2 && vdot(e1, e1) <= g2;
   tOut = 1000.f;
   if (!sc.all(ok)) return -1;

@@ -265,6 +265,37 @@ struct DevScene {
     return mat_at(mats + 8 * i);
   }
   __device__ __forceinline__ float refr(int i) const { return mats[8 * i + 7]; }
+  // The shading set-up's data of hit sphere i (>= 0): centre, guard radius^2
+  // and material.  When every active lane hit the same sphere (a coherent
+  // wave) they come through the scalar cache; otherwise per-lane gathers.
+  __device__ __forceinline__ void hit_data(int i, V3& c, float& g2, Mat& mt) const {
+    const int i0 = __builtin_amdgcn_readfirstlane(i);
+    if (__ballot(i != i0) == 0ull) {
+      const cfloat_p g = geom + 4 * i0;
+      c = v3(g[0], g[1], g[2]);
+      g2 = crad2[2 * n + (unsigned)i0];
+      mt = mat_at(mats + 8 * i0);
+    } else {
+      const float4 g = lgeom[i];
+      c = v3(g.x, g.y, g.z);
+      g2 = crad2[2 * n + (unsigned)i];
+      mt = mat_at(mats + 8 * i);
+    }
+  }
+  // Centre, r^2 and guard radius^2 of sphere h (>= 0), scalar when uniform.
+  __device__ __forceinline__ V3 sphere_guard(int h, float& r2, float& g2) const {
+    const int h0 = __builtin_amdgcn_readfirstlane(h);
+    if (__ballot(h != h0) == 0ull) {
+      const cfloat_p g = geom + 4 * h0;
+      r2 = g[3];
+      g2 = crad2[2 * n + (unsigned)h0];
+      return v3(g[0], g[1], g[2]);
+    }
+    const float4 g = lgeom[h];
+    r2 = g.w;
+    g2 = crad2[2 * n + (unsigned)h];
+    return v3(g.x, g.y, g.z);
+  }
   __device__ __forceinline__ void light(unsigned l, V3& pos, V3& col) const {
     cfloat_p p = lights + 6 * l;
     pos = v3(p[0], p[1], p[2]);

@@ -114,6 +114,16 @@ struct HostScene {
     return r;
   }
   float refr(int i) const { return mats[8 * i + 7]; }
+  void hit_data(int i, rtg::V3& c, float& g2, rtg::Mat& mt) const {
+    float r2;
+    c = sphere((unsigned)i, r2);
+    g2 = guard_r2((unsigned)i);
+    mt = mat(i);
+  }
+  rtg::V3 sphere_guard(int h, float& r2, float& g2) const {
+    g2 = guard_r2((unsigned)h);
+    return sphere((unsigned)h, r2);
+  }
   void light(unsigned l, rtg::V3& pos, rtg::V3& col) const {
     const float* p = lights + 6 * l;
     pos = rtg::v3(p[0], p[1], p[2]);
