@@ -657,31 +657,11 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 // f32 Fresnel and sinA1, and the return register zeroed by the reflection
 // push (:835-845), so a reflection child that leaves it stale returns 0 and a
 // leaf's colour is doubled once, not twice.
-// Reflection-ray prefetch (RTG_REFL_PREFETCH, A/B builds; results identical):
-// the reflection child rays live in private memory (scratch), and most of
-// their reads miss the L2, so a read at unwind stalls the next query for a
-// memory round trip.  The next ray the unwind will take is known as soon as a
-// node is known not to descend (miss, insignificant intensity, opaque hit or
-// leaf): it is the deepest level with a pending stage-1 reflection (`pend`
-// bit mask).  Its load is issued there, before the node's shading (shadow
-// rays, refraction factor), which covers the latency.
-#ifndef RTG_REFL_PREFETCH
-#define RTG_REFL_PREFETCH 0
-#endif
-
 template <int S, int Q, bool kCL = false, class Scene, class FStore>
 RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = false,
                        uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   FrameR fr[NF];                        // reflection child rays (private memory)
-#if RTG_REFL_PREFETCH
-  unsigned pend = 0;                    // bit lv: frame lv has a stage-1 reflection pending
-  FrameR pf;                            // the prefetched ray of the deepest pending level
-  pf.ro = pf.rd = pf.rI = v3(0.f, 0.f, 0.f);
-  auto prefetch = [&]() {
-    if (pend != 0u) pf = fr[31 - __builtin_clz(pend)];
-  };
-#endif
   int sp = 0;                           // == level of the node being processed
   V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
@@ -730,9 +710,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     sc.probe_end(kProbeClosest);
     sc.probe_begin(kProbeShade);
     if (hit < 0) {
-#if RTG_REFL_PREFETCH
-      if (RTG_REFL_PREFETCH == 1) prefetch();
-#endif
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
       sc.probe_begin(kProbeSplitSetup);
@@ -744,10 +721,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       const V3 N = vnorm(vsub(P, c));
       const float op = mh.opacity;
       const float tr = 1.f - op;
-#if RTG_REFL_PREFETCH
-      if (RTG_REFL_PREFETCH == 1 && (!(tr > 0.f) || sp >= S - 1))
-        prefetch();  // this node does not descend
-#endif
       V3 colour = v3(0.f, 0.f, 0.f);
       bool guardOK = false;
       if constexpr (Q == 4) {  // P in the hit sphere's guard ball (shadow/overlap masks)
@@ -797,10 +770,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             fr[lv].rd = rd;
             fr[lv].ro = vadd(P, vsmul(0.01f, rd));
             fr[lv].rI = rc;
-#if RTG_REFL_PREFETCH
-            pend |= 1u << lv;
-            if (RTG_REFL_PREFETCH == 2) pf = fr[lv];  // the new top, already in registers
-#endif
           }
           ++sp;
           ret = colour;                                       // :538
@@ -823,11 +792,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         ret = colour;
       }
     }
-#if RTG_REFL_PREFETCH
-    else if (RTG_REFL_PREFETCH == 1) {
-      prefetch();
-    }
-#endif
     // else: hit but insignificant intensity -> ret unchanged (stale)
     sc.probe_end(kProbeShade);
 
@@ -842,14 +806,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       if ((f.meta & 3u) == 2u) {                              // stage 1, reflection
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
-#if RTG_REFL_PREFETCH
-        o = pf.ro; d = pf.rd; I = pf.rI;                      // == fr[lv] (lv: pend's top bit)
-        pend &= ~(1u << lv);
-        if (RTG_REFL_PREFETCH == 2) prefetch();  // the next top, loaded ahead of its use
-#else
-        o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI;
-#endif
-        rm = (int)(f.meta >> 9);
+        o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 9);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
         descend = true;
