@@ -429,6 +429,16 @@ constexpr float kConeCos[kConeTiers] = {0.97814760073380569f,   // cos, rounded 
 // a kConeGrid x kConeGrid grid over the other two coordinates / |major|.  A
 // direction near a cell border may land in either cell; the masks' 1e-3 rad
 // margin covers that.
+// Reciprocal of the major-axis magnitude (> 0): the hardware approximation
+// (1 ulp) on the GPU; the cell only needs to be consistent with its border
+// margin, which is 1e-3 rad (a 1-ulp quotient moves a border by ~1e-7).
+RTG_HD float cone_rcp(float m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(m);
+#else
+  return 1.f / m;
+#endif
+}
 RTG_HD int cone_cell(V3 U) {
   const float ax = fabsf(U.x), ay = fabsf(U.y), az = fabsf(U.z);
   int face;
@@ -436,7 +446,7 @@ RTG_HD int cone_cell(V3 U) {
   if (ax >= ay && ax >= az) { face = U.x > 0.f ? 0 : 1; m = ax; a = U.y; b = U.z; }
   else if (ay >= az) { face = U.y > 0.f ? 2 : 3; m = ay; a = U.x; b = U.z; }
   else { face = U.z > 0.f ? 4 : 5; m = az; a = U.x; b = U.y; }
-  const float im = 1.f / m;
+  const float im = cone_rcp(m);
   int ia = (int)((a * im + 1.f) * (0.5f * kConeGrid));
   int ib = (int)((b * im + 1.f) * (0.5f * kConeGrid));
   ia = ia < 0 ? 0 : (ia > kConeGrid - 1 ? kConeGrid - 1 : ia);
@@ -1323,12 +1333,12 @@ RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
 // lexicographic minimum of (t, index) over h's root and the accepted roots
 // of the lane's mask spheres, which is what the index-order scan with strict
 // < keeps.
-template <class Scene>
+template <bool kFast, class Scene>
 RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
   float r2, g2;
   const V3 c = sc.sphere_guard(h, r2, g2);
   bool res;
-  const float th = ray_sphere(q, c, r2, res);
+  const float th = ray_sphere_k<kFast>(q, c, r2, res);
   const V3 e0 = vsub(q.o, c);
   const V3 e1 = vsub(vadd(q.o, vsmul(th, q.d)), c);
   ok = res && th < 1000.f && vdot(e0, e0) <= g2 && vdot(e1, e1) <= g2;
@@ -1345,7 +1355,7 @@ RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOu
     const V3 cj = sc.sphere(j, rj2);
     if ((own >> j) & 1ull) {
       bool rj;
-      const float t = ray_sphere(q, cj, rj2, rj);
+      const float t = ray_sphere_k<kFast>(q, cj, rj2, rj);
       if (rj && (t < minT || (t == minT && (int)j < best))) { minT = t; best = (int)j; }
     }
   }
@@ -1355,7 +1365,10 @@ RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOu
 
 template <class Scene>
 RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
-  if (sc.fuse & kFuseEnter) return closest_enter_fused(sc, q, h, tOut, ok);
+  if (sc.fuse & kFuseEnter) {
+    if (sc.all(q.fast)) return closest_enter_fused<true>(sc, q, h, tOut, ok);
+    return closest_enter_fused<false>(sc, q, h, tOut, ok);
+  }
   float r2;
   const V3 c = sc.sphere_lane((unsigned)h, r2);
   bool res;
