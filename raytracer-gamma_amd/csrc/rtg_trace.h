@@ -678,7 +678,19 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
   int rm = (int)sc.n;                   // background material
   int enterH = -1;  // Q == 4: the sphere this ray entered (refraction child), or -1
   int originH = -1;  // Q == 4: the sphere whose origin ball holds this ray's origin, or -1
+#if defined(__HIP_DEVICE_COMPILE__) && (defined(RTG_PAD_SALU) || defined(RTG_PAD_VALU))
+  unsigned padS;  // issue-cost probes (A/B builds only): dummy work per node
+  float padV;
+#endif
   for (;;) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_SALU)
+#pragma unroll
+    for (int k = 0; k < RTG_PAD_SALU; ++k) asm volatile("s_add_u32 %0, 7, 1" : "=s"(padS));
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_VALU)
+#pragma unroll
+    for (int k = 0; k < RTG_PAD_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, 2.0" : "=v"(padV));
+#endif
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
     sc.probe_begin(kProbeClosest);
@@ -825,6 +837,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       --sp;
     }
     sc.probe_end(kProbeUnwind);
+#if defined(__HIP_DEVICE_COMPILE__) && (defined(RTG_PAD_SALU) || defined(RTG_PAD_VALU))
+#endif
     if (!descend) return ret;
   }
 }
