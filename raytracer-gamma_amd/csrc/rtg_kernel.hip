@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   }
 }
 
-static TraceFn pick_trace(int S, bool lds, int variant, bool bvh, bool list) {
+static TraceFn pick_trace(int S, bool lds, int variant, bool bvh, int list) {
   switch (S) {
 #define RTG_CASE(k) case k: return trace_fn_s##k(lds, variant, bvh, list);
     RTG_CASE(1) RTG_CASE(2) RTG_CASE(3) RTG_CASE(4) RTG_CASE(5) RTG_CASE(6) RTG_CASE(7)
@@ -669,7 +669,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       grid = dim3(a.nPersist, 1);
     }
   }
-  TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr, listed);
+  // the compacted default kernel of a scene with shadow/overlap and cone masks
+  // takes them as compile-time facts (kMasks)
+  const int listKind = !listed ? 0 : (ctx->smask && ctx->cone) ? 2 : 1;
+  TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr, listKind);
   if (!fn) {
     rtg_set_error("no kernel for stackSize %d (valid: 1..%d), variant %d", stackSize,
                   RTG_MAX_STACK, variant);

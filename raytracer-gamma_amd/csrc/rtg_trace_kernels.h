@@ -49,8 +49,11 @@ struct LdsFrames {
 // kBvh: the kernel instantiation for BVH scenes (n > 64); without it the BVH
 // branches compile away, so small scenes keep the smaller, faster kernel.
 // kFuse: Scene::fuse bits (kFusePrim / kFuseCone / kFuseShadow, rtg_trace.h).
+// kMasks: the scene has shadow/overlap and cone masks (every finite scene of
+// <= 64 spheres, rtg_scene_pack.h), so has_smask() / has_cone() are
+// compile-time true and the kernel keeps no run-time flags for them.
 template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = false,
-          int kFuse = 0>
+          int kFuse = 0, bool kMasks = false>
 struct DevScene {
   static constexpr int fuse = kFuse;
   FrameC* lfr;
@@ -170,7 +173,10 @@ struct DevScene {
     return v3(first_lane(v.x), first_lane(v.y), first_lane(v.z));
   }
   // Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): n <= 64.
-  __device__ __forceinline__ bool has_cone() const { return cone != nullptr; }
+  __device__ __forceinline__ bool has_cone() const {
+    if constexpr (kMasks) return true;
+    else return cone != nullptr;
+  }
   // Union over the active lanes' origin spheres h (all >= 0) of cone mask
   // (h, tier, cell): one scalar load per distinct h.
   __device__ __forceinline__ uint64_t cone_union(int h, unsigned tier, unsigned cell) const {
@@ -186,7 +192,10 @@ struct DevScene {
     return u;
   }
   // Shadow and overlap masks (rtg_scene_pack.h shadow_masks): n <= 64.
-  __device__ __forceinline__ bool has_smask() const { return smask != nullptr; }
+  __device__ __forceinline__ bool has_smask() const {
+    if constexpr (kMasks) return true;
+    else return smask != nullptr;
+  }
   __device__ __forceinline__ uint64_t overlap_mask(unsigned h) const {  // per lane
     const cuint_p w = smask + 2u * (m * n + h);
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
@@ -688,12 +697,15 @@ struct SampleThreads {
 // guarantees a.groupList): the listed groups, dealt round-robin to the waves,
 // with the cull pass's sphere masks; otherwise K consecutive groups per wave.
 // Separate instantiations keep each loop's registers to itself.
-template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false>
+// kMasks (compacted default kernel only): the launcher guarantees the
+// scene's shadow/overlap and cone masks (DevScene).
+template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,
+          bool kMasks = false>
 __global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
 void trace_samples_kernel(const KernelArgs a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh, FuseOf<kVariant>::value> sc;
+  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh, FuseOf<kVariant>::value, kMasks> sc;
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
@@ -799,9 +811,14 @@ struct CompactVariant {
   static constexpr bool value = V == 0 || V == 15 || V == 17 || V == 18 || V == 19 || V == 20 ||
                                 V == 23 || V == 24 || V == 50 || V == 110;
 };
+// list: 0 the direct launch, 1 the compacted launch, 2 the compacted launch
+// of a scene with masks (kMasks instantiation of the default kernel).
 template <int S, int V>
-static TraceFn trace_fn_v(bool lds, bool list) {
+static TraceFn trace_fn_v(bool lds, int list) {
   if (list && !CompactVariant<V>::value) return nullptr;
+  if constexpr (V == 0) {
+    if (list == 2) return trace_samples_kernel<S, false, 0, false, true, true>;
+  }
   if constexpr (V == 17) {
     if (list)
       return lds ? trace_samples_kernel<S, true, V, false, true>
@@ -833,7 +850,7 @@ static TraceFn trace_fn_bvh(bool lds, int variant) {
   }
 }
 template <int S>
-static TraceFn trace_fn(bool lds, int variant, bool bvh, bool list) {
+static TraceFn trace_fn(bool lds, int variant, bool bvh, int list) {
   if (bvh) {
     if (list) return nullptr;  // BVH scenes (n > 64) are never compacted
     if (TraceFn f = trace_fn_bvh<S>(lds, variant)) return f;
@@ -870,7 +887,7 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh, bool list) {
 }
 
 // One per stack size, defined in rtg_trace_s<S>.hip.
-#define RTG_DECL(k) TraceFn trace_fn_s##k(bool lds, int variant, bool bvh, bool list);
+#define RTG_DECL(k) TraceFn trace_fn_s##k(bool lds, int variant, bool bvh, int list);
 RTG_DECL(1) RTG_DECL(2) RTG_DECL(3) RTG_DECL(4) RTG_DECL(5) RTG_DECL(6) RTG_DECL(7)
 RTG_DECL(8) RTG_DECL(9) RTG_DECL(10) RTG_DECL(11) RTG_DECL(12) RTG_DECL(13)
 RTG_DECL(14) RTG_DECL(15) RTG_DECL(16)

@@ -9,7 +9,7 @@
 #define RTG_CAT(a, b) RTG_CAT2(a, b)
 
 namespace rtg {
-TraceFn RTG_CAT(trace_fn_s, RTG_S)(bool lds, int variant, bool bvh, bool list) {
+TraceFn RTG_CAT(trace_fn_s, RTG_S)(bool lds, int variant, bool bvh, int list) {
   return trace_fn<RTG_S>(lds, variant, bvh, list);
 }
 }  // namespace rtg
