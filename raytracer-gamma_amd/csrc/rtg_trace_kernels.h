@@ -545,9 +545,23 @@ void trace_kernel(const KernelArgs a) {
 // rows, all their samples) traced by one wave, entered converged.
 // hasSel: the cull pass already gave the group's primary-ray sphere subset
 // (gsel, compacted launch), so the wave skips its own cull.
+// The kernel's argument block (the sample kernels' one by-value parameter, at
+// offset 0 of the kernarg segment) through an opaque pointer: each call's
+// field reads are fresh scalar loads where they are used, so the group set-up
+// and epilogue values are not held in SGPRs (or spilled to VGPR lanes) across
+// the whole trace.
+__device__ __forceinline__ const RTG_CONST KernelArgs* kargs() {
+  const RTG_CONST KernelArgs* p =
+      (const RTG_CONST KernelArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <int S, int Q, bool kDiag, class Sc, bool kShfl = false, bool kCL = false>
-__device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t gw,
+__device__ __forceinline__ void trace_group(const KernelArgs& a0, Sc& sc, size_t gw,
                                             bool hasSel = false, uint64_t gsel = 0) {
+  (void)a0;
+  const KernelArgs a = *kargs();  // == a0, read afresh for this group
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned SP = nAA * nAA;
@@ -629,13 +643,13 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
 #else
   if (valid) {
     c = trace_sample<S, Q, kCL>(sc, dir, sc.frames(), usePrim, primSel);
-    c = vsmul(a.cam.inv, c);
+    c = vsmul(kargs()->cam.inv, c);
   }
 #endif
   if constexpr (kDiag) {  // wave converged again: one add per slot
     sc.acc[kProbeTotal] = __builtin_amdgcn_s_memtime() - tk0;
     if ((threadIdx.x & 63u) == 0)
-      for (int k = 0; k < kProbeSlots; ++k) atomicAdd(&a.diag[k], sc.acc[k]);
+      for (int k = 0; k < kProbeSlots; ++k) atomicAdd(&kargs()->diag[k], sc.acc[k]);
   }
   // Ordered per-pixel sum (whole wave converged again): every lane parks its
   // sample in its own level-0 frame slot (LDS, free again: the trace is done)
@@ -667,7 +681,8 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a, Sc& sc, size_t 
     }
   }
   if (valid && s == 0) {
-    float* o = a.dst + ((size_t)lr * a.W + x) * 3;
+    const RTG_CONST KernelArgs* b = kargs();
+    float* o = b->dst + ((size_t)lr * b->W + x) * 3;
     o[0] = canon_nan(pix.x);
     o[1] = canon_nan(pix.y);
     o[2] = canon_nan(pix.z);
