@@ -37,6 +37,18 @@ constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 typedef const RTG_CONST float* cfloat_p;
 typedef const RTG_CONST unsigned* cuint_p;
 
+// Element i of a scene table with a 32-bit byte offset: base + zext(offset)
+// is what the scalar (s_load sbase, soffset) and vector (global_load v, saddr)
+// addressing modes take directly, so an index costs one 32-bit shift instead
+// of 64-bit shift/add/add-with-carry pairs.  Tables are far below 4 GiB.
+__device__ __forceinline__ cfloat_p fidx(cfloat_p p, unsigned i) {
+  return (cfloat_p)((const RTG_CONST char*)p + i * 4u);
+}
+__device__ __forceinline__ cuint_p uidx(cuint_p p, unsigned i) {
+  return (cuint_p)((const RTG_CONST char*)p + i * 4u);
+}
+__device__ __forceinline__ const float* fidx(const float* p, unsigned i) { return p + i; }
+
 // Per-lane frame colours in LDS: level lv of thread t at lfr[lv * kBlock + t]
 // (16-byte records, so a wave's ds_read_b128 covers 1 KiB contiguously and is
 // bank-conflict free).
@@ -111,15 +123,15 @@ struct DevScene {
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
   __device__ __forceinline__ V3 sphere(unsigned i, float& r2) const {
-    cfloat_p g = geom + 4 * i;
+    cfloat_p g = fidx(geom, 4 * i);
     r2 = g[3];
     return v3(g[0], g[1], g[2]);
   }
   // r^2 of sphere i (wave-uniform i: one scalar load)
-  __device__ __forceinline__ float sphere_r2(unsigned i) const { return geom[4 * i + 3]; }
+  __device__ __forceinline__ float sphere_r2(unsigned i) const { return fidx(geom, 4 * i)[3]; }
   // Four consecutive sphere records: one 64-byte scalar load.
   __device__ __forceinline__ void sphere4(unsigned i, V3* c, float* r2) const {
-    cfloat_p g = geom + 4 * i;
+    cfloat_p g = fidx(geom, 4 * i);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
@@ -185,7 +197,7 @@ struct DevScene {
     while (todo) {
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(h, src);
-      const cuint_p w = cone + 2u * (((unsigned)h0 * kConeTiers + tier) * kConeCells + cell);
+      const cuint_p w = uidx(cone, 2u * (((unsigned)h0 * kConeTiers + tier) * kConeCells + cell));
       u |= (uint64_t)w[0] | ((uint64_t)w[1] << 32);
       todo &= ~__ballot(h == h0);
     }
@@ -197,10 +209,10 @@ struct DevScene {
     else return smask != nullptr;
   }
   __device__ __forceinline__ uint64_t overlap_mask(unsigned h) const {  // per lane
-    const cuint_p w = smask + 2u * (m * n + h);
+    const cuint_p w = uidx(smask, 2u * (m * n + h));
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
-  __device__ __forceinline__ float guard_r2(unsigned i) const { return crad2[2 * n + i]; }
+  __device__ __forceinline__ float guard_r2(unsigned i) const { return *fidx(crad2, 2 * n + i); }
   // Union of the active lanes' overlap masks (one scalar load per distinct
   // h) and, in `own`, each lane's own mask.
   __device__ __forceinline__ uint64_t overlap_union(int h, uint64_t& own) const {
@@ -210,7 +222,7 @@ struct DevScene {
     while (todo) {
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(h, src);
-      const cuint_p w = smask + 2u * (m * n + (unsigned)h0);
+      const cuint_p w = uidx(smask, 2u * (m * n + (unsigned)h0));
       const uint64_t mk = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
       u |= mk;
       if (h == h0) own = mk;
@@ -229,7 +241,7 @@ struct DevScene {
     while (todo) {
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(hit, src);
-      const cuint_p w = smask + 2u * (row * n + (unsigned)h0);
+      const cuint_p w = uidx(smask, 2u * (row * n + (unsigned)h0));
       u |= (uint64_t)w[0] | ((uint64_t)w[1] << 32);
       todo &= ~__ballot(hit == h0);
     }
@@ -247,14 +259,14 @@ struct DevScene {
     r2 = g.w;
     return v3(g.x, g.y, g.z);
   }
-  __device__ __forceinline__ float contain_r2(unsigned i) const { return crad2[i]; }
+  __device__ __forceinline__ float contain_r2(unsigned i) const { return *fidx(crad2, i); }
   // primary_possible's per-sphere constants of sphere i
   __device__ __forceinline__ bool prim_possible(const PrimBundle& b, unsigned i, V3 c) const {
-    const cfloat_p k = prim + 4 * i;
+    const cfloat_p k = fidx(prim, 4 * i);
     return primary_possible(b, c, k[0], k[1], k[2]);
   }
   // |0 - c_i|^2 - r_i^2: the c term of a ray from the origin (primary rays)
-  __device__ __forceinline__ float origin_c(unsigned i) const { return crad2[n + i]; }
+  __device__ __forceinline__ float origin_c(unsigned i) const { return *fidx(crad2, n + i); }
   __device__ __forceinline__ Mat mat_at(decltype(mats) p) const {
     Mat r;
     r.matte = v3(p[0], p[1], p[2]);
@@ -269,44 +281,44 @@ struct DevScene {
   __device__ __forceinline__ Mat mat(int i) const {
     if constexpr (std::is_same<MatPtr, cfloat_p>::value) {
       const int i0 = __builtin_amdgcn_readfirstlane(i);
-      if (__ballot(i != i0) == 0ull) return mat_at(mats + 8 * i0);
+      if (__ballot(i != i0) == 0ull) return mat_at(fidx(mats, 8u * (unsigned)i0));
     }
-    return mat_at(mats + 8 * i);
+    return mat_at(fidx(mats, 8u * (unsigned)i));
   }
-  __device__ __forceinline__ float refr(int i) const { return mats[8 * i + 7]; }
+  __device__ __forceinline__ float refr(int i) const { return fidx(mats, 8u * (unsigned)i)[7]; }
   // The shading set-up's data of hit sphere i (>= 0): centre, guard radius^2
   // and material.  When every active lane hit the same sphere (a coherent
   // wave) they come through the scalar cache; otherwise per-lane gathers.
   __device__ __forceinline__ void hit_data(int i, V3& c, float& g2, Mat& mt) const {
     const int i0 = __builtin_amdgcn_readfirstlane(i);
     if (__ballot(i != i0) == 0ull) {
-      const cfloat_p g = geom + 4 * i0;
+      const cfloat_p g = fidx(geom, 4u * (unsigned)i0);
       c = v3(g[0], g[1], g[2]);
-      g2 = crad2[2 * n + (unsigned)i0];
-      mt = mat_at(mats + 8 * i0);
+      g2 = *fidx(crad2, 2 * n + (unsigned)i0);
+      mt = mat_at(fidx(mats, 8u * (unsigned)i0));
     } else {
-      const float4 g = lgeom[i];
-      c = v3(g.x, g.y, g.z);
-      g2 = crad2[2 * n + (unsigned)i];
-      mt = mat_at(mats + 8 * i);
+      const cfloat_p g = fidx(geom, 4u * (unsigned)i);
+      c = v3(g[0], g[1], g[2]);
+      g2 = *fidx(crad2, 2 * n + (unsigned)i);
+      mt = mat_at(fidx(mats, 8u * (unsigned)i));
     }
   }
   // Centre, r^2 and guard radius^2 of sphere h (>= 0), scalar when uniform.
   __device__ __forceinline__ V3 sphere_guard(int h, float& r2, float& g2) const {
     const int h0 = __builtin_amdgcn_readfirstlane(h);
     if (__ballot(h != h0) == 0ull) {
-      const cfloat_p g = geom + 4 * h0;
+      const cfloat_p g = fidx(geom, 4u * (unsigned)h0);
       r2 = g[3];
-      g2 = crad2[2 * n + (unsigned)h0];
+      g2 = *fidx(crad2, 2 * n + (unsigned)h0);
       return v3(g[0], g[1], g[2]);
     }
-    const float4 g = lgeom[h];
-    r2 = g.w;
-    g2 = crad2[2 * n + (unsigned)h];
-    return v3(g.x, g.y, g.z);
+    const cfloat_p g = fidx(geom, 4u * (unsigned)h);
+    r2 = g[3];
+    g2 = *fidx(crad2, 2 * n + (unsigned)h);
+    return v3(g[0], g[1], g[2]);
   }
   __device__ __forceinline__ void light(unsigned l, V3& pos, V3& col) const {
-    cfloat_p p = lights + 6 * l;
+    cfloat_p p = fidx(lights, 6 * l);
     pos = v3(p[0], p[1], p[2]);
     col = v3(p[3], p[4], p[5]);
   }
