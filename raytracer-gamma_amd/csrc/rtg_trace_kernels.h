@@ -47,7 +47,9 @@ __device__ __forceinline__ cfloat_p fidx(cfloat_p p, unsigned i) {
 __device__ __forceinline__ cuint_p uidx(cuint_p p, unsigned i) {
   return (cuint_p)((const RTG_CONST char*)p + i * 4u);
 }
+#if defined(__HIP_DEVICE_COMPILE__)  // (one type on the host pass, where RTG_CONST is empty)
 __device__ __forceinline__ const float* fidx(const float* p, unsigned i) { return p + i; }
+#endif
 
 // Per-lane frame colours in LDS: level lv of thread t at lfr[lv * kBlock + t]
 // (16-byte records, so a wave's ds_read_b128 covers 1 KiB contiguously and is
