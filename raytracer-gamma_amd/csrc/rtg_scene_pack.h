@@ -31,7 +31,9 @@ constexpr unsigned kMaskMaxSpheres = 64;
 // the shadow-ray masks' data, see shadow_masks).  geom: n x {x, y, z, r*r} followed by NaN padding
 // records up to n4 + 4 (n4 = n rounded up to 4), then the same n4 + 4 records
 // with the pass-1 screen radius^2 (screen_r2) in place of r*r, then with the
-// containment radius^2 (r + 1e-6f)^2 (primary_container); crad2: n x (r+1e-6)^2, then
+// containment radius^2 (r + 1e-6f)^2 (primary_container), then n4 + 4 32-byte
+// fused records {x, y, z, screen r^2, r^2, primary c term, 0, 0} (sphere_fused,
+// the fused query loops: one scalar load per sphere); crad2: n x (r+1e-6)^2, then
 // n x the primary-ray c term |0 - c|^2 - r^2 (same float operations and order
 // as the query's vdot(disp, disp) - r2 with disp = 0 - c, exact negation);
 // mats: (n+1) x {matte.xyz, gloss.xyz, opacity, n} with [n] = background
@@ -56,7 +58,7 @@ struct PackedScene {
   std::vector<float> bvhNodes, bvhAux;
   std::vector<int> bvhChild;
   unsigned n = 0, m = 0;
-  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records
+  unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records + the fused part
 };
 
 // Shadow-ray sphere masks.  A shadow ray of raytracer.h:272-309 starts at the
@@ -487,7 +489,9 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   ps->m = m;
   ps->n4 = (n + 3u) & ~3u;
   // Padding records are NaN spheres: their radicand is NaN, never >= 0.
-  ps->geom.assign((size_t)(ps->n4 + 4) * 12, __builtin_nanf(""));
+  // three parts of (n4 + 4) 16-byte records, then the fused part: (n4 + 4)
+  // 32-byte records {x, y, z, screen r^2, r^2, primary c term, 0, 0}
+  ps->geom.assign((size_t)(ps->n4 + 4) * 20, __builtin_nanf(""));
   ps->crad2.assign(n ? 3 * (size_t)n : 1, 0.f);
   ps->mats.assign((size_t)(n + 1) * 8, 0.f);
   ps->lights.assign((size_t)(m ? m : 1) * 6, 0.f);
@@ -508,6 +512,12 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     const float dx = 0.f - s.pos.x, dy = 0.f - s.pos.y, dz = 0.f - s.pos.z;
     ps->crad2[n + i] = (((dx * dx) + (dy * dy)) + (dz * dz)) - g[3];
     ps->crad2[2 * (size_t)n + i] = guard_r2(s);
+    float* gf = &ps->geom[(size_t)(ps->n4 + 4) * 12 + (size_t)i * 8];
+    gf[0] = g[0]; gf[1] = g[1]; gf[2] = g[2];
+    gf[3] = gs[3];
+    gf[4] = g[3];
+    gf[5] = ps->crad2[n + i];
+    gf[6] = 0.f; gf[7] = 0.f;
     prim_consts(s, &ps->prim[(size_t)i * 4]);
     float* mt = &ps->mats[(size_t)i * 8];
     mt[0] = s.material.matteColour.x; mt[1] = s.material.matteColour.y;

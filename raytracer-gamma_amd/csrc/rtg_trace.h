@@ -396,8 +396,9 @@ template <class Scene>
 RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel, float& nT) {
   int found = -1;
   nT = sc.refr((int)sc.n);  // background material (wave-uniform: scalar load)
-  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
+    m &= ~(1ull << i);  // s_bitset0
     float cr;
     const V3 c = sc.sphere_contain(i, cr);
     const float ni = sc.refr((int)i);  // scalar load, next to the record's
@@ -1280,11 +1281,11 @@ RTG_HD unsigned sign_mask(float v) {
 template <bool kFast, class Scene>
 RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_t sel) {
   bool blk = false;
-  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    float rs;
-    const V3 c = sc.sphere_screen(i, rs);
-    const float r2 = sc.sphere_r2(i);
+    m &= ~(1ull << i);  // s_bitset0
+    float rs, r2, ocu;
+    const V3 c = sc.sphere_fused(i, rs, r2, ocu);
     if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntShadowCand, 1);
       bool res;
@@ -1363,8 +1364,9 @@ RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOu
   own &= ~(1ull << h);
   float minT = th;
   int best = h;
-  for (uint64_t m = u; m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = u; m;) {  // wave-uniform
     const unsigned j = (unsigned)__builtin_ctzll(m);
+    m &= ~(1ull << j);  // s_bitset0
     float rj2;
     const V3 cj = sc.sphere(j, rj2);
     if ((own >> j) & 1ull) {
@@ -1424,11 +1426,11 @@ template <bool kFast, class Scene>
 RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
   float minT = 1000.f;
   int best = -1;
-  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    float rs;
-    const V3 c = sc.sphere_screen(i, rs);
-    const float r2 = sc.sphere_r2(i);
+    m &= ~(1ull << i);  // s_bitset0
+    float rs, r2, ocu;
+    const V3 c = sc.sphere_fused(i, rs, r2, ocu);
     if (!(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntFullCand, 1);
       bool res;
@@ -1447,8 +1449,9 @@ RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut
     return closest_sel_fused<false>(sc, q, sel, tOut);
   }
   uint64_t cand = 0;
-  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
+    m &= ~(1ull << i);  // s_bitset0
     float rs;
     const V3 c = sc.sphere_screen(i, rs);
     cand |= (pass1_rad(q, c, rs) < 0.f) ? 0ull : (1ull << i);
@@ -1481,12 +1484,13 @@ RTG_HD int closest_hit_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, f
   float minT = 1000.f;
   int best = -1;
   const V3 d = q.d;
-  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    float r2;
-    const V3 c = sc.sphere(i, r2);
+    m &= ~(1ull << i);  // s_bitset0
+    float rs, r2, oc;
+    const V3 c = sc.sphere_fused(i, rs, r2, oc);
     const float bp = 2.0f * vdot(d, c);
-    const float rad = (bp * bp) - (q.a4 * sc.origin_c(i));
+    const float rad = (bp * bp) - (q.a4 * oc);
     if (rad >= 0.0f) {
       sc.count(kCntPrimCand, 1);
       const float root = rtg_sqrtf(rad);
@@ -1517,8 +1521,9 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
   float minT = 1000.f;
   int best = -1;
   uint64_t cand = 0;
-  for (uint64_t m = sel; m; m &= m - 1) {  // wave-uniform: scalar loop + scalar loads
+  for (uint64_t m = sel; m;) {  // wave-uniform: scalar loop + scalar loads
     const unsigned i = (unsigned)__builtin_ctzll(m);
+    m &= ~(1ull << i);  // s_bitset0
     float r2;
     const V3 c = sc.sphere(i, r2);
     const float b = 2.0f * vdot(d, c);

@@ -151,6 +151,17 @@ struct DevScene {
   __device__ __forceinline__ V3 sphere_screen(unsigned i, float& rs) const {
     return sphere(n4 + 4 + i, rs);
   }
+  // Fused record of sphere i (geom's fourth part, 32 bytes: one
+  // s_load_dwordx8): centre, pass-1 screen radius^2, r^2 and the primary
+  // rays' c term |0 - c|^2 - r^2, for the fused query loops.
+  __device__ __forceinline__ V3 sphere_fused(unsigned i, float& rs, float& r2, float& oc) const {
+    typedef float f8 __attribute__((ext_vector_type(8)));
+    const f8 g = *(const RTG_CONST f8*)fidx(geom, 12 * (n4 + 4) + 8 * i);  // one load
+    rs = g[3];
+    r2 = g[4];
+    oc = g[5];
+    return v3(g[0], g[1], g[2]);
+  }
   __device__ __forceinline__ V3 sphere_contain(unsigned i, float& cr) const {
     return sphere(2 * (n4 + 4) + i, cr);
   }

@@ -66,6 +66,13 @@ struct HostScene {
   }
   rtg::V3 sphere_lane(unsigned i, float& r2) const { return sphere(i, r2); }
   float sphere_r2(unsigned i) const { return geom[4 * i + 3]; }
+  rtg::V3 sphere_fused(unsigned i, float& rs, float& r2, float& oc) const {
+    const float* g = geom + 12 * (n4 + 4) + 8 * i;
+    rs = g[3];
+    r2 = g[4];
+    oc = g[5];
+    return rtg::v3(g[0], g[1], g[2]);
+  }
   void probe_begin(int) const {}
   struct Frames {
     rtg::FrameC* f;
