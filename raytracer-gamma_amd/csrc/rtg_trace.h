@@ -139,8 +139,19 @@ RTG_HD float cull_rsq(float x) {
 #endif
 }
 RTG_HD float rtg_sqrtf(float x) { return sqrt_rn(x); }
+// rcp_rn(sqrt_rn(x)) with ONE range check: for x in sqrt_fast's range the
+// rounded root lies in [2^-48, 2^64], inside rcp_fast's, so both short
+// sequences hold; outside it, both compiler sequences (same results).
+RTG_HD float rcp_sqrt_rn(float x) {
+  float y = rcp_fast(sqrt_fast(x));
+  if (!sqrt_fast_range(x)) {
+    no_speculate();
+    y = 1.f / sqrtf(x);
+  }
+  return y;
+}
 // vec.h:41: l = 1.f / sqrt(dot); v *= l.
-RTG_HD V3 vnorm(V3 v) { float l = rcp_rn(rtg_sqrtf(vdot(v, v))); return vsmul(l, v); }
+RTG_HD V3 vnorm(V3 v) { float l = rcp_sqrt_rn(vdot(v, v)); return vsmul(l, v); }
 // raytracer.h:235-241
 RTG_HD bool significant(V3 c) { return (c.x >= 0.001f) || (c.y >= 0.001f) || (c.z >= 0.001f); }
 
@@ -239,7 +250,9 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.ap = a * (1.0f - 0x1p-16f);
   q.apB = a * (1.0f - kBoundK);
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
-  q.y = rcp_rn(q.den);
+  // y is used only when q.fast (quot, quot_k<true>); den is then in
+  // [2^-60, 2^60], inside rcp_fast's range, so no range check is needed.
+  q.y = rcp_fast(q.den);
   return q;
 }
 
@@ -476,7 +489,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
     sc.light(l, Lpos, Lcol);
     V3 dist = vsub(Lpos, P);
     const float gap = vdot(dist, dist);
-    const V3 dir = vsmul(rcp_rn(rtg_sqrtf(gap)), dist);  // vnorm(dist)
+    const V3 dir = vsmul(rcp_sqrt_rn(gap), dist);  // vnorm(dist)
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
       sc.probe_begin(kProbeShadow);

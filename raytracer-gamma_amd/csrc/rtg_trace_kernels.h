@@ -205,6 +205,11 @@ struct DevScene {
   // Union over the active lanes' origin spheres h (all >= 0) of cone mask
   // (h, tier, cell): one scalar load per distinct h.
   __device__ __forceinline__ uint64_t cone_union(int h, unsigned tier, unsigned cell) const {
+    const int hu = __builtin_amdgcn_readfirstlane(h);
+    if (__ballot(h != hu) == 0ull) {  // coherent wave: one origin sphere, one load
+      const cuint_p w = uidx(cone, 2u * (((unsigned)hu * kConeTiers + tier) * kConeCells + cell));
+      return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    }
     uint64_t todo = __ballot(1);
     uint64_t u = 0;
     while (todo) {
@@ -249,6 +254,11 @@ struct DevScene {
   // light l's shadow masks, row m the overlap masks.
   __device__ __forceinline__ uint64_t mask_union(unsigned row, int hit, bool ok) const {
     if (__ballot(!ok)) return n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+    const int hu = __builtin_amdgcn_readfirstlane(hit);
+    if (__ballot(hit != hu) == 0ull) {  // coherent wave: one hit sphere, one load
+      const cuint_p w = uidx(smask, 2u * (row * n + (unsigned)hu));
+      return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    }
     uint64_t todo = __ballot(1);
     uint64_t u = 0;
     while (todo) {
