@@ -234,6 +234,12 @@ struct DevScene {
   // Union of the active lanes' overlap masks (one scalar load per distinct
   // h) and, in `own`, each lane's own mask.
   __device__ __forceinline__ uint64_t overlap_union(int h, uint64_t& own) const {
+    const int hu = __builtin_amdgcn_readfirstlane(h);
+    if (__ballot(h != hu) == 0ull) {  // coherent wave: one sphere, one load
+      const cuint_p w = uidx(smask, 2u * (m * n + (unsigned)hu));
+      own = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      return own;
+    }
     uint64_t todo = __ballot(1);
     uint64_t u = 0;
     own = 0;
