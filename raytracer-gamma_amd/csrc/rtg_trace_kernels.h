@@ -755,10 +755,15 @@ struct SampleThreads {
 // Separate instantiations keep each loop's registers to itself.
 // kMasks (compacted default kernel only): the launcher guarantees the
 // scene's shadow/overlap and cone masks (DevScene).
+#ifdef RTG_NUM_SGPR  // A/B builds: SGPR budget of the sample kernels
+#define RTG_SGPR_ATTR __attribute__((amdgpu_num_sgpr(RTG_NUM_SGPR)))
+#else
+#define RTG_SGPR_ATTR
+#endif
 template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,
           bool kMasks = false>
 __global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
-void trace_samples_kernel(const KernelArgs a) {
+RTG_SGPR_ATTR void trace_samples_kernel(const KernelArgs a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
   DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh, FuseOf<kVariant>::value, kMasks> sc;
