@@ -755,15 +755,9 @@ struct SampleThreads {
 // Separate instantiations keep each loop's registers to itself.
 // kMasks (compacted default kernel only): the launcher guarantees the
 // scene's shadow/overlap and cone masks (DevScene).
-#ifdef RTG_NUM_SGPR  // A/B builds: SGPR budget of the sample kernels
-#define RTG_SGPR_ATTR __attribute__((amdgpu_num_sgpr(RTG_NUM_SGPR)))
-#else
-#define RTG_SGPR_ATTR
-#endif
-template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,
-          bool kMasks = false>
-__global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
-RTG_SGPR_ATTR void trace_samples_kernel(const KernelArgs a) {
+// The body of the sample kernels (one per launch kind below).
+template <int S, bool kLds, int kVariant, bool kBvh, bool kList, bool kMasks>
+__device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
   DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh, FuseOf<kVariant>::value, kMasks> sc;
@@ -795,6 +789,30 @@ RTG_SGPR_ATTR void trace_samples_kernel(const KernelArgs a) {
                                                                                  gw * K + k);
   }
   record_wave(a, t0, gw);
+}
+
+template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,
+          bool kMasks = false>
+__global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
+void trace_samples_kernel(const KernelArgs a) {
+  trace_samples_body<S, kLds, kVariant, kBvh, kList, kMasks>(a);
+}
+
+// The compacted default kernel of a masked scene with an SGPR budget
+// (amdgpu_num_sgpr): on gfx950 a wave's SGPR allocation sets the resident-wave
+// ceiling below the register allocator's model (tools/ubench/occ.hip: an SGPR
+// count of 86-94 allows 7 waves per SIMD, 100+ only 6).  78 requested SGPRs
+// (76 with VCC etc.) admit 8 waves, with 61 VGPRs and 5 KB of LDS per wave; the
+// extra SGPR spills to VGPR lanes cost less than the eighth wave gains
+// (A/B C3 1.755 vs 1.780 ms, C4 11.05 vs 11.35; resident waves per SIMD mean
+// 7.1, peak 7.8, vs 6.4 / 6.8).  Instantiated for S <= 6 (trace_fn_v).
+#ifndef RTG_NUM_SGPR
+#define RTG_NUM_SGPR 78
+#endif
+template <int S>
+__global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_sgpr(RTG_NUM_SGPR)))
+void trace_samples_kernel_masked(const KernelArgs a) {
+  trace_samples_body<S, false, 0, false, true, true>(a);
 }
 
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
@@ -878,7 +896,12 @@ template <int S, int V>
 static TraceFn trace_fn_v(bool lds, int list) {
   if (list && !CompactVariant<V>::value) return nullptr;
   if constexpr (V == 0) {
-    if (list == 2) return trace_samples_kernel<S, false, 0, false, true, true>;
+    if (list == 2) {
+      // S <= 6: the SGPR-budgeted 8-wave kernel; deeper stacks hold more LDS
+      // per wave than 8 waves per SIMD admit anyway
+      if constexpr (S <= 6) return trace_samples_kernel_masked<S>;
+      else return trace_samples_kernel<S, false, 0, false, true, true>;
+    }
   }
   if constexpr (V == 17) {
     if (list)
