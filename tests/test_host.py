@@ -223,3 +223,17 @@ def test_host_driver_scene_options(tmp_path):
         pytest.skip("rtg_main not built")
     r = subprocess.run([exe, "--help"], capture_output=True, text=True)
     assert "--scene" in r.stdout and "--gpus" in r.stdout
+
+
+def test_short_sequence_ranges_compose():
+    """rcp_sqrt_rn (rtg_trace.h) takes rcp(sqrt(x)) with sqrt_fast's range check
+    only, and make_query takes the reciprocal of 2|d|^2 with none: both rely on
+    the rounded root / the Markstein denominator lying inside rcp_fast's range
+    [2^-125, 2^125].  Check those bounds at the range ends in binary32."""
+    f = np.float32
+    lo, hi = f(2.0 ** -96), np.finfo(np.float32).max
+    for x in (lo, np.nextafter(lo, f(1)), f(1), np.nextafter(hi, f(0)), hi):
+        s = np.sqrt(f(x), dtype=np.float32)
+        assert f(2.0 ** -125) <= s <= f(2.0 ** 125), (x, s)
+    # the kFast quotient's denominator range (RayQ::fast) inside rcp_fast's
+    assert 2.0 ** -125 <= 2.0 ** -60 and 2.0 ** 60 <= 2.0 ** 125
