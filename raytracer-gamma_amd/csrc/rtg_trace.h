@@ -113,19 +113,29 @@ RTG_HD void no_speculate() {
   asm volatile("");
 #endif
 }
+// Whether any active lane needs the fallback: a wave-uniform test, so the
+// common case costs one compare-to-mask and a scalar branch, with no exec-mask
+// save/restore around the (skipped) fallback.
+RTG_HD bool any_lane(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ballot_w64(b) != 0ull;
+#else
+  return b;
+#endif
+}
 RTG_HD float sqrt_rn(float x) {
   float s = sqrt_fast(x);
-  if (!sqrt_fast_range(x)) {
+  if (any_lane(!sqrt_fast_range(x))) {
     no_speculate();
-    s = sqrtf(x);
+    if (!sqrt_fast_range(x)) s = sqrtf(x);
   }
   return s;
 }
 RTG_HD float rcp_rn(float b) {
   float y = rcp_fast(b);
-  if (!rcp_fast_range(b)) {
+  if (any_lane(!rcp_fast_range(b))) {
     no_speculate();
-    y = 1.f / b;
+    if (!rcp_fast_range(b)) y = 1.f / b;
   }
   return y;
 }
@@ -144,9 +154,9 @@ RTG_HD float rtg_sqrtf(float x) { return sqrt_rn(x); }
 // sequences hold; outside it, both compiler sequences (same results).
 RTG_HD float rcp_sqrt_rn(float x) {
   float y = rcp_fast(sqrt_fast(x));
-  if (!sqrt_fast_range(x)) {
+  if (any_lane(!sqrt_fast_range(x))) {
     no_speculate();
-    y = 1.f / sqrtf(x);
+    if (!sqrt_fast_range(x)) y = 1.f / sqrtf(x);
   }
   return y;
 }
