@@ -559,21 +559,23 @@ RTG_HD double sqrt_d_unit(double y) {
 }
 RTG_HD double div_d_fresnel(double a, double b, bool fast) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (fast) {
-    double y = __builtin_amdgcn_rcp(b);
-    double e = fma(-b, y, 1.0);
-    y = fma(y, e, y);
-    e = fma(-b, y, 1.0);
-    y = fma(y, e, y);
-    const double q = a * y;
-    const double r = fma(-b, q, a);
-    return fma(r, y, q);
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  const double q = a * y;
+  const double r = fma(-b, q, a);
+  double d = fma(r, y, q);
+  if (any_lane(!fast)) {  // wave-uniform test: the rare fallback
+    no_speculate();
+    if (!fast) d = a / b;
   }
-  no_speculate();
+  return d;
 #else
   (void)fast;
-#endif
   return a / b;
+#endif
 }
 
 // raytracer.h:370-403 (f64 island).  kCL: the OpenCL kernel's all-float
@@ -594,11 +596,14 @@ RTG_HD float polarised_reflection(float n1, float n2, float cosA1, float cosA2) 
   const double num = (double)(left - right);
   double den = (double)(left + right);
   den *= den;
-  if (den < (double)1.0e-6f) return 1.f;
+  // den < 1e-6: the reference returns 1 without dividing (raytracer.h:387-391);
+  // here the quotient of those lanes is computed and discarded (a select, not
+  // a divergent early return)
+  const bool tiny = den < (double)1.0e-6f;
   const bool fast = fabsf(left) <= 0x1p100f && fabsf(right) <= 0x1p100f;
-  float refl = (float)div_d_fresnel(num * num, den, fast);
+  float refl = (float)div_d_fresnel(num * num, den, fast || tiny);
   if (refl > 1.f) refl = 1.f;
-  return refl;
+  return tiny ? 1.f : refl;
 }
 
 // raytracer.h:642-815.  Computes the reflection factor R and, when wantRay,
