@@ -13,10 +13,13 @@ and rank 0 gathers them with one RCCL gather over xGMI and restores row order
 on the device, so the step ends with the whole frame in rank 0's HBM (strong
 scaling: fixed frame).  Rank 0 prints one JSON line.
 
-Also reported: the kernel roofline (FP32 VALU; algorithmic work = the
-reference's ray-sphere tests x 25 flops), the reference CPU
-path timed on a bounded row sample on this host (cpu_baseline), and parity of
-the produced frame/PPM against the reference's golden hashes.
+Also reported: the kernel roofline (VALU issue; work = the VALU operations the
+kernel EXECUTES, counted per wave by the counting build of the same kernel,
+rtg_amd/work.py; the reference's brute-force test count x 25 flops beside it
+as `reference_work`), end-to-end frame times (scene preparation + upload,
+render, read-back, PPM bytes), the reference CPU path timed on a bounded
+pixel sample on this host (cpu_baseline), and parity of the produced
+frame/PPM against the reference's golden hashes.
 """
 from __future__ import annotations
 
@@ -36,6 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "raytracer-gamma_amd"))
 import rtg_amd as R  # noqa: E402
 from rtg_amd import dist as rdist  # noqa: E402
+from rtg_amd import work as rwork  # noqa: E402
 
 METRIC = "Mpixels/s (primary rays) + frame ms at WxH, depth D; PPM max-abs-diff vs CPU"
 GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.json")
@@ -46,11 +50,12 @@ CONFIGS = {  # name: (W, H, spheres, lights, depth)  — BASELINE.json configs
     "c4": (7680, 4320, 32, 4, 5),
     "c5": (3840, 2160, 1024, 4, 7),
 }
-# FP32 VALU issue peak for non-FMA ops: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
-# (MI355X_MICROARCH.md's 157.3 TFLOPS FP32-vector spec counts an FMA as two
-# flops; parity with the reference forbids contraction, so adds and muls issue
-# separately and 78.6 T op/s is the ceiling for this kernel's op mix.)
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# VALU issue peak: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz = one wave64 VALU
+# instruction per 2 cycles per SIMD (MI355X_MICROARCH.md: CDNA4 SIMDs are
+# 32 wide; its 157.3 TFLOPS FP32 spec counts an FMA as two flops, and parity
+# with the reference forbids contraction, so 78.6 T op/s is this kernel's
+# ceiling).  BASELINE.md's 39.3 T assumed SIMD-16, which gfx950 is not.
+VALU_PEAK_TOPS = rwork.VALU_PEAK_TOPS
 HBM_PEAK_GBS = 8000.0
 FLOPS_PER_TEST = 25  # raySphere pre-branch ops, SURVEY.md §8d
 
@@ -77,50 +82,55 @@ def cpu_threads() -> int:
 
 def cpu_baseline(name, sph, lg, W, H, S, budget_s):
     """The reference CPU path (oracle/_ref, compiled from the reference's own
-    raytracer.h) over a strided row sample of the same frame, on one host
-    thread (the reference's main.cpp:404 loop is single-threaded) and on all
-    host threads with dynamic row scheduling; falls back to
-    the C restatement if the reference build is absent.  Each leg gets half
-    of `budget_s` of wall time.  The multi-threaded figure is the baseline."""
+    raytracer.h) over a seeded uniform random sample of the frame's pixels,
+    on one host thread (the reference's main.cpp:404 loop is single-threaded)
+    and on all host threads; falls back to the C restatement
+    (rows) if the reference build is absent.  Each leg gets half of
+    `budget_s`: a 256-pixel calibration run sizes the sample to fill it (C5's
+    pixels cost ~1000x C3's).  The multi-threaded figure is the baseline; the
+    frame time is extrapolated from the sample."""
     ref = os.path.join(ROOT, "oracle", "_ref", f"librtgref_S{S}.so")
     port = os.path.join(ROOT, "oracle", "build", "librtg_oracle.so")
     kind = "reference" if os.path.exists(ref) else "port"
     L = ctypes.CDLL(ref if kind == "reference" else port)
     P = lambda a: ctypes.c_void_p(a.ctypes.data) if a.size else None  # noqa: E731
+    rng = np.random.default_rng(7)
+    perm = rng.permutation(W * H).astype(np.uint32)  # a prefix of it is a uniform sample
 
-    def run(rows, threads):
-        rows = np.asarray(rows, np.uint32)
+    def run(n, threads):
+        if kind == "reference":
+            gids = np.sort(perm[:n])
+            out = np.zeros((n, 3), np.float32)
+            t0 = time.perf_counter()
+            L.ref_render_pixels(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
+                                ctypes.c_float(3.0), P(gids), n, P(out), threads)
+            return time.perf_counter() - t0, gids, out
+        rows = np.sort(rng.choice(H, size=max(1, n // W), replace=False)).astype(np.uint32)
         out = np.zeros((len(rows), W, 3), np.float32)
         t0 = time.perf_counter()
-        if kind == "reference":
-            L.ref_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
-                              ctypes.c_float(3.0), P(rows), len(rows), P(out), threads)
-        else:
-            L.oracle_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
-                                 ctypes.c_float(3.0), S, P(rows), len(rows), P(out), threads,
-                                 None)
-        return time.perf_counter() - t0, out
+        L.oracle_render_rows(P(sph), len(sph), P(lg), len(lg), W, H, ctypes.c_float(-4.0),
+                             ctypes.c_float(3.0), S, P(rows), len(rows), P(out), threads, None)
+        gids = (rows[:, None].astype(np.int64) * W + np.arange(W)).reshape(-1)
+        return time.perf_counter() - t0, gids, out.reshape(-1, 3)
 
     def leg(threads, budget):
-        # calibrate on a 1/64 stride, then pick the stride that fits the budget
-        t_cal, _ = run(range(0, H, 64), threads)
-        stride = max(1, int(np.ceil(t_cal * 64 / budget)))
-        rows = list(range(0, H, stride))
-        t, out = run(rows, threads)
-        px = len(rows) * W
+        t_cal, _, _ = run(256, threads)
+        n = int(min(W * H, max(256, 256 * budget / max(t_cal, 1e-6))))
+        t, gids, out = run(n, threads)
+        px = len(gids)
         return {"value": round(px / t / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
                 "kind": kind,
-                "sample": f"{name} rows 0,{stride},{2 * stride},... ({len(rows)} of {H} rows, "
-                          f"{px} px, {t:.1f} s, {threads} thread{'s' if threads > 1 else ''})",
-                "frame_s_extrapolated": round(t * H / len(rows), 1)}, rows, out
+                "sample": f"{name}: {px} pixels drawn uniformly from the {W}x{H} frame (seed 7)"
+                          f", {t:.1f} s on {threads} thread{'s' if threads > 1 else ''}",
+                "frame_s_extrapolated": round(t * W * H / px, 1)}, gids, out
 
     T = cpu_threads()
-    one, rows, out = leg(1, budget_s / 2)
+    one, g1, o1 = leg(1, budget_s / 2)
     if T > 1:
-        multi, rows_m, out_m = leg(T, budget_s / 2)
+        multi, gm, om = leg(T, budget_s / 2)
         multi["single_thread"] = one
-        return multi, rows + rows_m, np.concatenate([out, out_m])
-    return one, rows, out
+        return multi, np.concatenate([g1, gm]), np.concatenate([o1, om])
+    return one, g1, o1
 
 
 def main():
@@ -140,6 +150,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=16.0,
                     help="seconds of CPU baseline (split between the 1-thread and all-thread legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-work-count", action="store_true",
+                    help="skip the counting-build run (executed-work roofline); PMC passes use "
+                         "this so that only the timed kernel is profiled")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end frame timings")
     ap.add_argument("--gather-chunks", type=int, default=4,
                     help="N > 1: split each rank's rows into K chunks; each chunk is rendered "
                          "then gathered asynchronously, so RCCL overlaps the next chunk's "
@@ -168,7 +182,12 @@ def main():
     B = args.row_block
     sph, lg = R.generate_scene(n, m, 42)
     ctx = R.Context(local)
-    ctx.set_scene(sph, lg)
+    t_scene = []
+    for _ in range(3 if world == 1 else 1):  # host preparation + upload, blocking
+        t0 = time.perf_counter()
+        ctx.set_scene(sph, lg)
+        t_scene.append((time.perf_counter() - t0) * 1e3)
+    scene_stats = ctx.scene_stats()
     if args.variant:
         ctx.set_variant(args.variant)
 
@@ -330,12 +349,16 @@ def main():
         rows = g["rows"]["rows"]
         want = np.fromfile(rows_file, np.float32).reshape(len(rows), W, 3)
         diffs.append((fb[rows], want))
+    if "wide" in g:  # C5's widened reference sample (tests/golden/make_c5_wide.py)
+        z = np.load(os.path.join(ROOT, "tests", "golden", g["wide"]["file"]))
+        diffs.append((fb[z["rows"].astype(np.int64)], z["rows_fb"]))
+        diffs.append((fb.reshape(-1, 3)[z["gids"].astype(np.int64)], z["pixels"]))
 
     # ---------------- CPU baseline (rank 0, N = 1 only)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu, crow, cout = cpu_baseline(args.config, sph, lg, W, H, S, args.cpu_budget)
-        diffs.append((fb[crow], cout))
+        cpu, cgid, cout = cpu_baseline(args.config, sph, lg, W, H, S, args.cpu_budget)
+        diffs.append((fb.reshape(-1, 3)[cgid], cout))
     if diffs:
         a = np.concatenate([d[0].reshape(-1) for d in diffs])
         b = np.concatenate([d[1].reshape(-1) for d in diffs])
@@ -343,31 +366,113 @@ def main():
         ok = ~(nan_a | nan_b)
         parity["max_abs_diff_float"] = float(np.max(np.abs(a[ok] - b[ok]))) if ok.any() else 0.0
         parity["nan_positions_match"] = bool((nan_a == nan_b).all())
+        parity["bit_exact"] = bool(parity["nan_positions_match"] and np.array_equal(
+            a[ok].view(np.uint32), b[ok].view(np.uint32)))
         parity["values_compared"] = int(a.size)
         # PPM bytes of those pixels under the frame's max colour
         mx = R.max_colour_value(fb)
         pa, pb = R.ppm_bytes(a.reshape(-1, 3), mx), R.ppm_bytes(b.reshape(-1, 3), mx)
         parity["ppm_max_abs_diff"] = int(np.max(np.abs(pa.astype(int) - pb.astype(int))))
 
+    # ---------------- executed work (counting build of the timed kernel)
+    # Variant 120 runs the default kernel's control flow with per-wave unit
+    # counters (rtg_amd/work.py); one frame, after the timed region.
+    work = None
+    if world == 1 and not args.no_work_count and args.variant == 0:
+        ctx.set_variant(120)
+        ctx.diag_counts(reset=True)
+        ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, stream=sptr)
+        torch.cuda.synchronize()
+        wv, lv = ctx.diag_counts(reset=True)
+        ctx.set_variant(args.variant)
+        work = rwork.executed_work(R.UNIT_NAMES, wv, lv)
+        work["counters"] = {nm: [int(wv[k]), int(lv[k])] for k, nm in enumerate(R.UNIT_NAMES)
+                            if not nm.startswith("U.")}
+
+    # ---------------- end to end (N = 1): the reference's per-run flow
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        host = torch.empty((H, W, 3), dtype=torch.float32, pin_memory=True)
+        mxd = torch.empty(1, dtype=torch.float32, device="cuda")
+        ppm_d = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
+        ppm_h = torch.empty(H * W * 3, dtype=torch.uint8, pin_memory=True)
+        t_full, t_d2h, t_ppm = [], [], []
+        for _ in range(3):
+            # scene upload (main.cpp:277-294) + render and finish (:353-374) +
+            # read-back of the float frame (:460)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.set_scene(sph, lg)
+            ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, stream=sptr)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            host.copy_(shard[:H], non_blocking=True)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            t_full.append((t2 - t0) * 1e3)
+            t_d2h.append((t2 - t1) * 1e3)
+            # resident scene: render, device max + PPM bytes (algebra.h:68-91,
+            # main.cpp:66-81), read-back of the 3 B/px image
+            t0 = time.perf_counter()
+            ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, stream=sptr)
+            ctx.max_colour_device(shard.data_ptr(), W * H, mxd.data_ptr(), stream=sptr)
+            ctx.ppm_bytes_device(shard.data_ptr(), W * H, mxd.data_ptr(), ppm_d.data_ptr(),
+                                 stream=sptr)
+            ppm_h.copy_(ppm_d, non_blocking=True)
+            torch.cuda.synchronize()
+            t_ppm.append((time.perf_counter() - t0) * 1e3)
+        e2e = {"e2e_ms": round(float(np.median(t_full)), 3),
+               "scene_prep_ms": round(float(np.median(t_scene)), 3),
+               "scene_host_prep_ms": round(scene_stats["prep_ms"], 3),
+               "scene_upload_ms": round(scene_stats["upload_ms"], 3),
+               "scene_device_bytes": scene_stats["device_bytes"],
+               "bvh_nodes": scene_stats["bvh_nodes"],
+               "render_ms": round(kern_ms, 4),
+               "d2h_fb_ms": round(float(np.median(t_d2h)), 3),
+               "e2e_ppm_resident_scene_ms": round(float(np.median(t_ppm)), 3),
+               "note": "e2e_ms = set_scene (host masks/BVH + H2D) + render + D2H of the "
+                       f"{W * H * 12 / 1e6:.1f} MB float frame into pinned memory (main.cpp:277-"
+                       "294, 353-374, 460); e2e_ppm_resident_scene_ms = render + device max + "
+                       "PPM bytes + D2H of 3 B/px; medians of 3"}
+
     # ---------------- roofline (rank-0 launch)
     tests = g.get("ray_sphere_tests")
     roof = None
-    if tests:
-        frac_rows = my_rows / H  # exact for N = 1; row-proportional estimate for N > 1
-        flops = tests * FLOPS_PER_TEST * frac_rows
-        ach = flops / (kern_ms * 1e-3) / 1e12
+    hbm = {"achieved_GBs": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9, 2),
+           "peak_GBs": HBM_PEAK_GBS,
+           "frac": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+           "algorithmic_bytes": my_rows * W * 12}
+    if work is not None:
+        ach = work["lane_ops"] / (kern_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "TFLOP/s", "frac": round(ach / VALU_PEAK_TOPS, 4), "traffic": None,
-                "work": f"{tests} reference ray-sphere tests x {FLOPS_PER_TEST} FP32 ops "
-                        f"x {frac_rows:.4f} of rows, / mean kernel time {kern_ms:.3f} ms (HIP events "
-                        f"on the launch stream around the timed launches)",
-                "hbm": {"achieved_GBs": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9, 2),
-                        "peak_GBs": HBM_PEAK_GBS,
-                        "frac": round(my_rows * W * 12 / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
-                        "algorithmic_bytes": my_rows * W * 12}}
-        # HBM traffic per launch from the committed PMC passes (tools/gpu_pmc.sh ->
-        # profiles/pmc_<config>.json), used only when measured on these kernel
-        # sources, this variant and N = 1.
+                "work": f"{work['lane_ops']:.4g} executed VALU lane-ops per frame = 64 x "
+                        f"{work['valu_slots']:.4g} wave-instruction slots, counted per wave by "
+                        "the counting build (variant 120) and priced per unit "
+                        "(rtg_amd/work.py), / mean kernel time "
+                        f"{kern_ms:.3f} ms (HIP events on the launch stream)",
+                "executed_valu_slots": work["valu_slots"],
+                "units": {k: v for k, v in sorted(work["units"].items(),
+                                                  key=lambda kv: -kv[1]["slots"]) if v["waves"]},
+                "counters": work["counters"],
+                "hbm": hbm}
+        if tests:
+            roof["reference_work"] = {
+                "flop": tests * FLOPS_PER_TEST,
+                "note": f"{tests} ray-sphere tests of the reference's brute-force scans x "
+                        f"{FLOPS_PER_TEST} FP32 ops (SURVEY.md §8d)"}
+            roof["work_avoided_ratio"] = round(tests * FLOPS_PER_TEST / work["lane_ops"], 3)
+    elif tests:  # no counting run: the reference's test count only, labelled as such
+        flops = tests * FLOPS_PER_TEST * my_rows / H
+        roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "TFLOP/s", "frac": None, "traffic": None,
+                "reference_work": {"flop": flops, "per_s_T": round(flops / (kern_ms * 1e-3) / 1e12, 3),
+                                   "note": "reference brute-force tests x 25 (not executed work)"},
+                "hbm": hbm}
+    if roof is not None:
+        # HBM traffic and VALU issue per launch from the committed PMC passes
+        # (tools/gpu_pmc.sh -> profiles/pmc_<config>.json), used only when
+        # measured on these kernel sources, this variant and N = 1.
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(pmc) and world == 1:
             rec = json.load(open(pmc))
@@ -381,8 +486,12 @@ def main():
                 roof["traffic"] = int(rec["traffic_bytes"])
                 if "valu_issue_utilisation" in rec:
                     roof["valu_issue_utilisation_pmc"] = round(rec["valu_issue_utilisation"], 3)
+                vi = rec.get("counters", {}).get("SQ_INSTS_VALU")
+                if vi and work is not None:
+                    roof["pmc_valu_insts"] = int(vi)
+                    roof["model_vs_pmc_valu"] = round(work["valu_slots"] / vi, 3)
                 roof["traffic_note"] = ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
-                                        f"({pmc}); mostly private-memory reflection rays")
+                                        f"({os.path.relpath(pmc, ROOT)})")
 
     out = {
         "metric": METRIC, "value": round(mpx, 2), "unit": "Mpixels/s", "n_gpus": world,
@@ -398,7 +507,7 @@ def main():
                         else " + gloo gather") if world > 1 else "")},
         "mrays_per_s": round(mpx * 9, 1),
         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
-        "roofline": roof, "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu, "e2e": e2e,
         "gpu_vs_cpu": round(mpx / cpu["value"], 1) if cpu else None,
         "parity": parity,
         "ab": ab,

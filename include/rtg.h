@@ -45,6 +45,10 @@ extern "C" {
 
 #define RTG_ABI_VERSION 1
 #define RTG_MAX_STACK 16 /* largest supported RTSTACK_MAXSIZE */
+/* Scenes hold fewer than RTG_MAX_SPHERES spheres (rtg_context_set_scene
+ * rejects larger ones with RTG_ERR_INVALID): the kernel keeps sphere and
+ * material indices in 23-bit fields and 32-bit table offsets. */
+#define RTG_MAX_SPHERES (1u << 23)
 
 /* vec.h:27-29 */
 typedef struct rtg_vec { float x, y, z; } rtg_vec;
@@ -122,6 +126,12 @@ int rtg_context_destroy(rtg_context* ctx);
 int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned sphNum,
                           const rtg_light* lights, unsigned lgtNum);
 
+/* Cost of the last rtg_context_set_scene (end-to-end reporting, SURVEY.md
+ * §8d): out4 = {host preparation ms (packed records, shadow / overlap / cone
+ * masks, BVH build), upload ms (device allocation + H2D copies), device bytes
+ * of the scene, BVH nodes}.  Zeros before the first scene. */
+int rtg_context_scene_stats(rtg_context* ctx, double* out4);
+
 /* Row sharding.  Rows are grouped in blocks of `rowBlock` rows; block b belongs
  * to shard (b % nShards) (row-cyclic).  A shard's rows are
  * packed in increasing row order.  nShards == 1 gives the whole frame in
@@ -182,6 +192,12 @@ int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts);
  * {closest-hit queries, shadow queries, refraction, whole pixel} into 8
  * counters; read (and optionally zero) them.  Zeros for normal variants. */
 int rtg_diag_read(rtg_context* ctx, unsigned long long* out8, int reset);
+/* Executed-work counters of the counting build (variant 120: the default
+ * kernel's control flow with per-unit counters): out[0 .. n/2)
+ * wave-level executions of each unit (rtg_trace.h kCnt* / kU* slots), out[n/2
+ * .. n) lane-level sums.  Copies min(cap, n) values, optionally zeroes them,
+ * and returns n (cap <= 0: just returns n); negative on error. */
+int rtg_diag_counts(rtg_context* ctx, unsigned long long* out, int cap, int reset);
 #define RTG_LAUNCH_TIMELINE 1 /* record a per-wave timeline (rtg_diag_timeline) */
 /* Wave timeline of the last launch made with RTG_LAUNCH_TIMELINE: one record
  * per wave {start, end (s_memrealtime, 100 MHz, low 32 bits), HW_ID, XCC_ID},

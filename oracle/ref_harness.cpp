@@ -138,6 +138,36 @@ void ref_render_rows(const void* spheres, unsigned sphNum, const void* lights,
   }
 }
 
+// Render the listed pixels (gid = y * W + x, each < W * H) into out[k*3 ..]:
+// the sampled-pixel fixtures of configs too slow to render whole (C5).
+void ref_render_pixels(const void* spheres, unsigned sphNum, const void* lights,
+                       unsigned lgtNum, unsigned W, unsigned H, float zoom,
+                       float aliasFactor, const unsigned* gids, unsigned npx,
+                       float* out, int nthreads) {
+  std::vector<struct Sphere> sph(sphNum);
+  std::vector<struct Light> lgt(lgtNum);
+  if (sphNum) std::memcpy(sph.data(), spheres, sphNum * sizeof(struct Sphere));
+  if (lgtNum) std::memcpy(lgt.data(), lights, lgtNum * sizeof(struct Light));
+  std::atomic<unsigned> next(0);
+  auto worker = [&]() {
+    for (;;) {
+      const unsigned k0 = next.fetch_add(64);  // 64 pixels per grab
+      if (k0 >= npx) break;
+      const unsigned k1 = k0 + 64 < npx ? k0 + 64 : npx;
+      for (unsigned k = k0; k < k1; ++k)
+        shade_pixel(sph.data(), sphNum, lgt.data(), lgtNum, W, H, zoom, aliasFactor, gids[k],
+                    out + (size_t)k * 3);
+    }
+  };
+  if (nthreads <= 1) {
+    worker();
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t) pool.emplace_back(worker);
+    for (auto& t : pool) t.join();
+  }
+}
+
 // algebra.h:68-91, called directly.
 float ref_max_colour(const float* fb, unsigned long long npx) {
   return maxColourValuePixelBuffer((const Vec*)fb, (size_t)npx);

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <type_traits>
 #include <vector>
 
@@ -236,6 +237,7 @@ struct rtg_context {
   int* bvhChild = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
+  unsigned long long* counts = nullptr;  // unit counters of the counting build (variant 120)
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
   // Compacted-launch scratch: a ring of slots, so that renders of one
   // context on different streams can overlap; a slot is reused only after
@@ -256,6 +258,9 @@ struct rtg_context {
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
   bool hasScene = false;
+  // the last rtg_context_set_scene: host preparation ms (records, masks,
+  // cone masks, BVH), upload ms, device bytes, BVH nodes (rtg_context_scene_stats)
+  double sceneStats[4] = {0, 0, 0, 0};
 };
 
 using namespace rtg;
@@ -375,6 +380,7 @@ int rtg_context_destroy(rtg_context* ctx) {
   free_scene(ctx);
   (void)hipFree(ctx->maxScratch);
   (void)hipFree(ctx->diag);
+  (void)hipFree(ctx->counts);
   (void)hipFree(ctx->timeline);
   for (auto& sl : ctx->slots) {
     (void)hipFree(sl.list);
@@ -399,6 +405,32 @@ int rtg_diag_read(rtg_context* ctx, unsigned long long* out, int reset) {
   HIP_TRY(hipMemcpy(out, ctx->diag, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   if (reset) HIP_TRY(hipMemset(ctx->diag, 0, 8 * sizeof(unsigned long long)));
   return RTG_OK;
+}
+
+int rtg_context_scene_stats(rtg_context* ctx, double* out4) {
+  rtg_clear_error();
+  if (!ctx || !out4) return RTG_ERR_INVALID;
+  for (int k = 0; k < 4; ++k) out4[k] = ctx->hasScene ? ctx->sceneStats[k] : 0.0;
+  return RTG_OK;
+}
+
+int rtg_diag_counts(rtg_context* ctx, unsigned long long* out, int cap, int reset) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
+  rtg_clear_error();
+  if (!ctx || (cap > 0 && !out)) return RTG_ERR_INVALID;
+  const int n = 2 * kCntSlots;
+  if (cap <= 0) return n;
+  const int k = cap < n ? cap : n;
+  if (!ctx->counts) {
+    for (int i = 0; i < k; ++i) out[i] = 0;
+    return n;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, ctx->counts, (size_t)k * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  if (reset) HIP_TRY(hipMemset(ctx->counts, 0, (size_t)n * sizeof(unsigned long long)));
+  return n;
 }
 
 int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* count) {
@@ -448,10 +480,21 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     rtg_set_error("rtg_context_set_scene: invalid arguments");
     return RTG_ERR_INVALID;
   }
+  // Table limits of the kernel: a frame record keeps the refractive material
+  // index in 23 bits (FrameC::meta, rm << 9), and scene tables are addressed
+  // with 32-bit byte offsets (fidx / uidx; the fused records end at 80 n
+  // bytes).  Both hold for n < RTG_MAX_SPHERES.
+  if (sphNum >= RTG_MAX_SPHERES) {
+    rtg_set_error("rtg_context_set_scene: %u spheres (at most %u)", sphNum, RTG_MAX_SPHERES - 1);
+    return RTG_ERR_INVALID;
+  }
   HIP_TRY(hipSetDevice(ctx->device));
   free_scene(ctx);
+  using clk = std::chrono::steady_clock;
+  const auto tPack = clk::now();
   PackedScene ps;
   pack_scene(spheres, sphNum, lights, lgtNum, &ps);
+  const auto tUp = clk::now();
   std::vector<float4> geom(ps.geom.size() / 4);
   memcpy(geom.data(), ps.geom.data(), ps.geom.size() * sizeof(float));
   const std::vector<float>& crad2 = ps.crad2;
@@ -516,6 +559,15 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
   ctx->hasScene = true;
+  const auto tEnd = clk::now();
+  ctx->sceneStats[0] = std::chrono::duration<double, std::milli>(tUp - tPack).count();
+  ctx->sceneStats[1] = std::chrono::duration<double, std::milli>(tEnd - tUp).count();
+  ctx->sceneStats[2] = (double)((ps.geom.size() + ps.crad2.size() + ps.mats.size() +
+                                 ps.lights.size() + ps.prim.size() + ps.bvhNodes.size() +
+                                 ps.bvhAux.size()) * sizeof(float) +
+                                (ps.smask.size() + ps.cone.size()) * sizeof(unsigned) +
+                                ps.bvhChild.size() * sizeof(int));
+  ctx->sceneStats[3] = (double)(ps.bvhChild.size() / 4);
   return RTG_OK;
 }
 
@@ -553,7 +605,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
   if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 20 ||
       variant == 21 || variant == 22 || variant == 23 || variant == 24 || variant == 50 ||
-      variant == 110)
+      variant == 110 || variant == 120)
     ldsMats = false;
   unsigned rows;
   if (rowList) {
@@ -597,12 +649,19 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.rowList = rowList;
   a.dst = reinterpret_cast<float*>(dstDevice);
   a.diag = nullptr;
+  a.counts = nullptr;
   a.timeline = nullptr;
   a.groupList = nullptr;
   a.groupSel = nullptr;
   a.groupCount = nullptr;
   a.nPersist = 0;
-  if (variant >= 100) {
+  if (variant == 120) {  // executed-work counting build
+    if (!ctx->counts) {
+      HIP_TRY(hipMalloc(&ctx->counts, 2 * kCntSlots * sizeof(unsigned long long)));
+      HIP_TRY(hipMemset(ctx->counts, 0, 2 * kCntSlots * sizeof(unsigned long long)));
+    }
+    a.counts = ctx->counts;
+  } else if (variant >= 100) {
     if (!ctx->diag) {
       HIP_TRY(hipMalloc(&ctx->diag, 8 * sizeof(unsigned long long)));
       HIP_TRY(hipMemset(ctx->diag, 0, 8 * sizeof(unsigned long long)));
@@ -613,6 +672,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
   rtg_context::GroupSlot* slot = nullptr;  // compacted launch scratch
   bool listed = false;                     // compacted launch (kList kernel)
+  size_t cullGroups = 0;                   // pixel groups of the cull pass
   if (sampleKernel) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
     const size_t groupsPerWave = variant == 21 ? 4 : 1;
@@ -650,12 +710,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         slot->cap = groups;
       }
       if (!slot->count) HIP_TRY(hipMalloc(&slot->count, sizeof(unsigned)));
-      HIP_TRY(hipMemsetAsync(slot->count, 0, sizeof(unsigned), (hipStream_t)stream));
-      hipLaunchKernelGGL(cull_groups_kernel,
-                         dim3((unsigned)((groups + 256 * kCullRounds - 1) / (256 * kCullRounds))),
-                         dim3(256), 0, (hipStream_t)stream, a, groups, slot->list, slot->sel,
-                         slot->count);
-      HIP_TRY(hipGetLastError());
+      cullGroups = groups;  // the cull pass is enqueued below, after the last failure point
       // about one wave per listed group: the benchmark scenes list 13-17 % of
       // their groups; a wave past the count exits at once, and a scene that
       // lists more deals up to five groups to each wave
@@ -695,9 +750,25 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     ctx->timelineCount = waves;
     a.timeline = ctx->timeline;
   }
+  // Stream work starts here, after every check and allocation that can fail,
+  // so an error never leaves a cull pass (which zero-fills dst and fills the
+  // slot's list) in flight without the slot's event behind it.
+  if (slot) {
+    HIP_TRY(hipMemsetAsync(slot->count, 0, sizeof(unsigned), (hipStream_t)stream));
+    hipLaunchKernelGGL(
+        cull_groups_kernel,
+        dim3((unsigned)((cullGroups + 256 * kCullRounds - 1) / (256 * kCullRounds))), dim3(256),
+        0, (hipStream_t)stream, a, cullGroups, slot->list, slot->sel, slot->count);
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+      hipLaunchKernelGGL(fn, grid, dim3(threads), lds, (hipStream_t)stream, a);
+    (void)hipEventRecord(slot->done, (hipStream_t)stream);  // on every path
+    HIP_TRY(e);
+    HIP_TRY(hipGetLastError());
+    return RTG_OK;
+  }
   hipLaunchKernelGGL(fn, grid, dim3(threads), lds, (hipStream_t)stream, a);
   HIP_TRY(hipGetLastError());
-  if (slot) HIP_TRY(hipEventRecord(slot->done, (hipStream_t)stream));
   return RTG_OK;
 }
 

@@ -183,11 +183,47 @@ enum : int { kFusePrim = 1, kFuseCone = 2, kFuseShadow = 4, kFuseEnter = 8 };
 
 // Diagnostic probe slots (scenes without probes implement them as no-ops).
 // Operation counters (host simulation only; sc.count is a no-op on the GPU).
+// The kU* slots are the executed-work units of the roofline:
+// one count per execution of a code unit; the device counting build (kernel
+// variant 120, DevScene kCount) sums them per WAVE (a unit some lane of the
+// wave executes costs the whole wave its instructions) and per lane.
 enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, kCntEnterOK,
              kCntFullQ, kCntFullCand, kCntShadowQ, kCntShadowSel, kCntShadowCand,
              kCntContainMasked, kCntContainSel, kCntContainFull, kCntRefraction, kCntReflPush,
              kCntBvhNodeTests, kCntBvhSphereTests, kCntConeQ, kCntConeSel,
-             kCntBvhShadowQ, kCntBvhShadowNodeTests, kCntBvhShadowSphereTests, kCntSlots };
+             kCntBvhShadowQ, kCntBvhShadowNodeTests, kCntBvhShadowSphereTests,
+             kUQuery,       // make_query: a, 4a, 2a, screen factors, 1/2a
+             kUPrimIter,    // closest_hit_sel_fused: one sphere's primary radicand
+             kUPrimExact,   // ... its root test (sqrt, two quotients, accept, best)
+             kUSelIter,     // closest_sel_fused: pass-1 screen of one sphere
+             kUSelExact,    // ... exact root test + closest update
+             kUShdIter,     // blocked_sel_fused: pass-1 screen of one sphere
+             kUShdExact,    // ... exact root test + blocking test
+             kUEnterHead,   // closest_enter_fused: sphere h's root test + guard tests
+             kUEnterIter,   // ... one overlap sphere, loaded
+             kUEnterExact,  // ... its root test + lexicographic update
+             kUFullGroup,   // candidate_mask: pass-1 screens of 4 spheres
+             kUFullExact,   // closest_hit_mask / blocked_mask: one candidate's root test
+             kUBvhNode,     // BVH node visit: pop, records, front-to-back push
+             kUBvhSlot,     // BVH slot: distance prune + bound / sphere screen
+             kUBvhExact,    // BVH leaf sphere: root test + update (closest or shadow)
+             kUContIter,    // primary_container_sel: one sphere's containment test
+             kUCont4,       // primary_container: 4 spheres' containment tests
+             kUContBvhNode, // container_bvh: one node (4 slots)
+             kUCone,        // cone cull set-up (bundle axis, tier, cell)
+             kUMaskIter,    // mask-union waterfall step (distinct sphere of the wave)
+             kUNode,        // stage-0 node: query dispatch, miss / hit bookkeeping
+             kUShade,       // significant hit: P, N, guard test, material, colour
+             kULight,       // matte_light: one light's direction and incidence
+             kUShadow,      // a shadow ray's query set-up (incidence > 0)
+             kULit,         // an unblocked light's intensity and sum
+             kURefr,        // refraction with the refracted ray (interior node)
+             kURefrLeaf,    // refraction without the ray (leaf: R and target only)
+             kUPush,        // reflection child ray (calculateReflection) + frame write
+             kUDescend,     // descent to the refraction child (frame, I, o, d)
+             kUUnwind,      // one unwind step (stage 1/2 colour sums)
+             kUSample,      // one primary sample: ray set-up, cull hand-over, pixel sum
+             kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
              kProbeSlots = 8 };
@@ -387,6 +423,7 @@ RTG_HD int primary_container(const Scene& sc, V3 pt) {
   int found = -1;
   const unsigned n4 = sc.n4;
   for (unsigned k = 0; k < n4; k += 4) {  // wave-uniform
+    sc.count(kUCont4, 1);
     V3 c[4];
     float cr[4];
     sc.sphere4_contain(k, c, cr);
@@ -422,6 +459,7 @@ RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel, float& nT
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
     m &= ~(1ull << i);  // s_bitset0
+    sc.count(kUContIter, 1);
     float cr;
     const V3 c = sc.sphere_contain(i, cr);
     const float ni = sc.refr((int)i);  // scalar load, next to the record's
@@ -495,6 +533,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
   V3 sum = v3(0.f, 0.f, 0.f);
   const unsigned m = sc.m;
   for (unsigned l = 0; l < m; ++l) {
+    sc.count(kULight, 1);
     V3 Lpos, Lcol;
     sc.light(l, Lpos, Lcol);
     V3 dist = vsub(Lpos, P);
@@ -502,6 +541,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
     const V3 dir = vsmul(rcp_sqrt_rn(gap), dist);  // vnorm(dist)
     const float incidence = vdot(N, dir);
     if (incidence > 0.f) {
+      sc.count(kUShadow, 1);
       sc.probe_begin(kProbeShadow);
       bool blk;
       if constexpr (Q == 4) {
@@ -518,6 +558,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
       }
       sc.probe_end(kProbeShadow);
       if (!blk) {
+        sc.count(kULit, 1);
         const float intensity = incidence / gap;
         sum = vadd(sum, vsmul(intensity, Lcol));
       }
@@ -722,6 +763,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
 #endif
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
+    sc.count(kUNode, 1);
     sc.probe_begin(kProbeClosest);
     int hit;
     if (usePrim) {  // the primary ray: only spheres its wave's bundle can reach
@@ -732,6 +774,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     } else if (Q == 4 && sc.has_smask() && sc.all(enterH >= 0)) {
       // every active lane traces a ray that entered a sphere: try h + overlaps
       bool ok;
+      sc.count(kUQuery, 1);
       hit = closest_enter(sc, make_query(o, d), enterH, t, ok);
       sc.count(kCntEnterQ, 1);
       sc.count(kCntEnterOK, ok ? 1 : 0);
@@ -739,6 +782,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     } else if (Q == 4 && sc.has_cone() && sc.all(originH >= 0)) {
       // secondary rays from sphere origin balls in a narrow bundle: only the
       // spheres of their cone masks for the bundle's cell
+      sc.count(kUCone, 1);
       const V3 dh = vsmul(cull_rsq(vdot(d, d)), d);  // about unit length
       const V3 U = sc.first_lane(dh);
       const float cu = vdot(dh, U);
@@ -747,6 +791,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         const uint64_t cm = sc.cone_union(originH, (unsigned)tier, (unsigned)cone_cell(U));
         sc.count(kCntConeQ, 1);
         sc.count(kCntConeSel, __builtin_popcountll(cm));
+        sc.count(kUQuery, 1);
         hit = closest_sel(sc, make_query(o, d), cm, t);
       } else {
         sc.count(kCntFullQ, 1);
@@ -763,6 +808,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     if (hit < 0) {
       ret = vmul(I, sc.mat(rm).matte);                       // :544
     } else if (significant(I)) {                             // :460
+      sc.count(kUShade, 1);
       sc.probe_begin(kProbeSplitSetup);
       V3 c;
       float g2;
@@ -795,6 +841,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         float R;
         sc.probe_begin(kProbeRefraction);
         sc.count(kCntRefraction, 1);
+        sc.count(leaf ? kURefrLeaf : kURefr, 1);
         const int tgt = Q == 4 ? refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R, hit, guardOK)
                                : refraction<kCL>(sc, d, P, N, mr.refr, !leaf, cdir, R);
         sc.probe_end(kProbeRefraction);
@@ -815,6 +862,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
                    ((unsigned)(sc.has_cone() && guardOK ? hit + 1 : 0) << 2) | (sigR ? 2u : 0u);
           if (sigR) {
             sc.count(kCntReflPush, 1);
+            sc.count(kUPush, 1);
             // calculateReflection, raytracer.h:817-842
             const float perp = 2.f * vdot(d, N);
             const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
@@ -822,6 +870,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             fr[lv].ro = vadd(P, vsmul(0.01f, rd));
             fr[lv].rI = rc;
           }
+          sc.count(kUDescend, 1);
           ++sp;
           ret = colour;                                       // :538
           // refraction child: calculateRefraction's refracted ray (:805-809);
@@ -850,6 +899,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     sc.probe_begin(kProbeUnwind);
     bool descend = false;
     while (sp > 0) {
+      sc.count(kUUnwind, 1);
       const int lv = sp - 1 < NF ? sp - 1 : NF - 1;
       FrameC& f = fc(lv);
       const V3 fcol = vadd(ret, v3(f.cx, f.cy, f.cz));        // :553 / :622
@@ -1121,6 +1171,7 @@ RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool activ
     pk[k] = 0.f;
     const int x = ch[k];
     if (x == 0) continue;  // wave-uniform
+    sc.count(kUBvhSlot, 1);
     const V3 p = vsub(q.o, c[k]);
     const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
@@ -1150,8 +1201,10 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
   st.push(0);
   while (!st.empty()) {  // wave-uniform
     const unsigned nd = (unsigned)st.pop();
+    sc.count(kUBvhNode, 1);
     bvh_ray_node(sc, q, nd, true, minT * dn, st, [&](unsigned i) {
       sc.count(kCntFullCand, 1);
+      sc.count(kUBvhExact, 1);
       float r2;
       const V3 ce = sc.sphere(i, r2);
       bool res;
@@ -1176,8 +1229,10 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   while (!st.empty()) {  // wave-uniform
     if (sc.all(blk)) break;
     const unsigned nd = (unsigned)st.pop();
+    sc.count(kUBvhNode, 1);
     bvh_ray_node(sc, q, nd, !blk, reach, st, [&](unsigned i) {
       sc.count(kCntShadowCand, 1);
+      sc.count(kUBvhExact, 1);
       float r2;
       const V3 ce = sc.sphere(i, r2);
       bool res;
@@ -1201,6 +1256,7 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
   st.push(0);
   while (!st.empty()) {  // wave-uniform
     const int nd = st.pop();
+    sc.count(kUContBvhNode, 1);
     V3 c[4];
     float w[4], rp[4], cr[4];
     int ch[4];
@@ -1228,6 +1284,7 @@ RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, con
   // records past n are NaN padding (PackedScene), masked off below.
   unsigned neg = 0;
   for (int k = (int)((cnt + 3u) & ~3u) - 4; k >= 0; k -= 4) {
+    sc.count(kUFullGroup, 1);
     V3 c[4];
     float r2[4];
     sc.sphere4_screen(base + (unsigned)k, c, r2);
@@ -1241,6 +1298,7 @@ RTG_HD unsigned candidate_mask(const Scene& sc, unsigned base, unsigned cnt, con
 
 template <class Scene>
 RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
+  sc.count(kUQuery, 1);
   const RayQ q = make_query(o, d);
   if (sc.has_bvh()) return closest_bvh(sc, q, tOut);
   float minT = 1000.f;
@@ -1253,6 +1311,7 @@ RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
       sc.count(kCntFullCand, 1);
+      sc.count(kUFullExact, 1);
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;
@@ -1267,6 +1326,7 @@ RTG_HD int closest_hit_mask(const Scene& sc, V3 o, V3 d, float& tOut) {
 // Shadow query with the two-pass scheme; stops at the first blocker.
 template <class Scene>
 RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
+  sc.count(kUQuery, 1);
   const RayQ q = make_query(o, d);
   if (sc.has_bvh()) return blocked_bvh(sc, q, gap);
   const unsigned n = sc.n;
@@ -1276,6 +1336,7 @@ RTG_HD bool blocked_mask(const Scene& sc, V3 o, V3 d, float gap) {
     while (mask) {
       const unsigned i = base + (unsigned)lowest_bit(mask);
       mask &= mask - 1;
+      sc.count(kUFullExact, 1);
       float r2;
       const V3 c = sc.sphere_lane(i, r2);
       bool res;
@@ -1312,10 +1373,12 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
     m &= ~(1ull << i);  // s_bitset0
+    sc.count(kUShdIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
     if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntShadowCand, 1);
+      sc.count(kUShdExact, 1);
       bool res;
       const float t = ray_sphere_k<kFast>(q, c, r2, res);
       if (res && t < 1000.f) {
@@ -1330,6 +1393,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
 
 template <class Scene>
 RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
+  sc.count(kUQuery, 1);
   const RayQ q = make_query(o, d);
   if (sc.fuse & kFuseShadow) {
     if (sc.all(q.fast)) return blocked_sel_fused<true>(sc, q, gap, sel);
@@ -1378,6 +1442,7 @@ RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
 // < keeps.
 template <bool kFast, class Scene>
 RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
+  sc.count(kUEnterHead, 1);
   float r2, g2;
   const V3 c = sc.sphere_guard(h, r2, g2);
   bool res;
@@ -1395,9 +1460,11 @@ RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOu
   for (uint64_t m = u; m;) {  // wave-uniform
     const unsigned j = (unsigned)__builtin_ctzll(m);
     m &= ~(1ull << j);  // s_bitset0
+    sc.count(kUEnterIter, 1);
     float rj2;
     const V3 cj = sc.sphere(j, rj2);
     if ((own >> j) & 1ull) {
+      sc.count(kUEnterExact, 1);
       bool rj;
       const float t = ray_sphere_k<kFast>(q, cj, rj2, rj);
       if (rj && (t < minT || (t == minT && (int)j < best))) { minT = t; best = (int)j; }
@@ -1457,10 +1524,12 @@ RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
     m &= ~(1ull << i);  // s_bitset0
+    sc.count(kUSelIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
     if (!(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntFullCand, 1);
+      sc.count(kUSelExact, 1);
       bool res;
       const float t = ray_sphere_k<kFast>(q, c, r2, res);
       if (res && t < minT) { minT = t; best = (int)i; }
@@ -1515,12 +1584,14 @@ RTG_HD int closest_hit_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, f
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
     m &= ~(1ull << i);  // s_bitset0
+    sc.count(kUPrimIter, 1);
     float rs, r2, oc;
     const V3 c = sc.sphere_fused(i, rs, r2, oc);
     const float bp = 2.0f * vdot(d, c);
     const float rad = (bp * bp) - (q.a4 * oc);
     if (rad >= 0.0f) {
       sc.count(kCntPrimCand, 1);
+      sc.count(kUPrimExact, 1);
       const float root = rtg_sqrtf(rad);
       const float u0 = quot_k<kFast>(bp + root, q);
       const float u1 = quot_k<kFast>(bp - root, q);
@@ -1537,6 +1608,7 @@ RTG_HD int closest_hit_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, f
 
 template <class Scene>
 RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t sel) {
+  sc.count(kUQuery, 1);
   const RayQ q = make_query(o, d);
   // The primary ray starts at the origin (main.cpp:417): disp = 0 - c = -c
   // exactly, so b = 2 d.disp = -(2 d.c) and b*b is (2 d.c)^2; the c term

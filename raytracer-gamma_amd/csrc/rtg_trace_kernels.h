@@ -66,8 +66,13 @@ struct LdsFrames {
 // kMasks: the scene has shadow/overlap and cone masks (every finite scene of
 // <= 64 spheres, rtg_scene_pack.h), so has_smask() / has_cone() are
 // compile-time true and the kernel keeps no run-time flags for them.
+// kCount: the executed-work counting build (kernel variant 120): count()
+// accumulates every unit (rtg_trace.h kCnt* / kU*) per lane and, once per
+// wave-level execution, on the wave's first active lane; flush_counts() adds
+// the wave's sums to KernelArgs::counts.  Control flow is the default
+// kernel's, so the counts are the default kernel's executed work.
 template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = false,
-          int kFuse = 0, bool kMasks = false>
+          int kFuse = 0, bool kMasks = false, bool kCount = false>
 struct DevScene {
   static constexpr int fuse = kFuse;
   FrameC* lfr;
@@ -108,7 +113,42 @@ struct DevScene {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  __device__ __forceinline__ void count(int, long) const {}  // host simulation only
+  mutable unsigned cntW[kCount ? kCntSlots : 1];  // wave-level executions (first active lane)
+  mutable unsigned cntL[kCount ? kCntSlots : 1];  // lane-level sum of the counted values
+  __device__ __forceinline__ void count_reset() const {
+    if constexpr (kCount)
+      for (int k = 0; k < kCntSlots; ++k) cntW[k] = cntL[k] = 0u;
+  }
+  __device__ __forceinline__ void count(int slot, long v) const {
+    if constexpr (kCount) {
+      const uint64_t act = __ballot(1);
+      const unsigned lane = threadIdx.x & 63u;
+      cntW[slot] += (lane == (unsigned)__builtin_ctzll(act)) ? 1u : 0u;
+      cntL[slot] += (unsigned)v;
+    } else {
+      (void)slot;
+      (void)v;
+    }
+  }
+  // Adds the wave's counters to out[0 .. kCntSlots) (wave-level) and
+  // out[kCntSlots .. 2 kCntSlots) (lane-level); whole wave converged.
+  __device__ __forceinline__ void flush_counts(unsigned long long* out) const {
+    if constexpr (kCount) {
+      for (int k = 0; k < kCntSlots; ++k) {
+        unsigned w = cntW[k], l = cntL[k];
+        for (int off = 32; off > 0; off >>= 1) {
+          w += __shfl_xor(w, off);
+          l += __shfl_xor(l, off);
+        }
+        if ((threadIdx.x & 63u) == 0) {
+          if (w) atomicAdd(&out[k], (unsigned long long)w);
+          if (l) atomicAdd(&out[kCntSlots + k], (unsigned long long)l);
+        }
+      }
+    } else {
+      (void)out;
+    }
+  }
   cfloat_p geom;      // n x {x, y, z, r*r}
   cfloat_p crad2;
   MatPtr mats;        // LDS copy (float*) or the global table (cfloat_p)
@@ -213,6 +253,7 @@ struct DevScene {
     uint64_t todo = __ballot(1);
     uint64_t u = 0;
     while (todo) {
+      count(kUMaskIter, 1);
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(h, src);
       const cuint_p w = uidx(cone, 2u * (((unsigned)h0 * kConeTiers + tier) * kConeCells + cell));
@@ -244,6 +285,7 @@ struct DevScene {
     uint64_t u = 0;
     own = 0;
     while (todo) {
+      count(kUMaskIter, 1);
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(h, src);
       const cuint_p w = uidx(smask, 2u * (m * n + (unsigned)h0));
@@ -268,6 +310,7 @@ struct DevScene {
     uint64_t todo = __ballot(1);
     uint64_t u = 0;
     while (todo) {
+      count(kUMaskIter, 1);
       const int src = __builtin_ctzll(todo);
       const int h0 = __builtin_amdgcn_readlane(hit, src);
       const cuint_p w = uidx(smask, 2u * (row * n + (unsigned)h0));
@@ -380,6 +423,7 @@ struct KernelArgs {
   const unsigned* groupCount;
   unsigned nPersist;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
+  unsigned long long* counts;  // 2 x kCntSlots unit counters (counting build, variant 120)
   uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
 };
 
@@ -428,7 +472,8 @@ template <int S, int kVariant>
 #endif
 struct MinWaves {
   static constexpr int value =
-      (kVariant == 18 && S <= 6) ? 8
+      (kVariant == 120) ? 1  // counting build: its counters take registers
+      : (kVariant == 18 && S <= 6) ? 8
       : (kVariant == 0 && S <= 6) ? RTG_DEFAULT_MIN_WAVES
       : ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
 };
@@ -683,6 +728,7 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a0, Sc& sc, size_t
   c = vsmul(a.cam.inv, v3(dir.x, (float)__builtin_popcountll(primSel), 0.f));
 #else
   if (valid) {
+    sc.count(kUSample, 1);
     c = trace_sample<S, Q, kCL>(sc, dir, sc.frames(), usePrim, primSel);
     c = vsmul(kargs()->cam.inv, c);
   }
@@ -730,6 +776,17 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a0, Sc& sc, size_t
   }
 }
 
+// Diagnostic builds: 100 + v are s_memtime probe builds of v (kDiag); 120 is
+// the executed-work counting build of the default kernel (kCount).
+template <int V>
+struct IsCount {
+  static constexpr bool value = V == 120;
+};
+template <int V>
+struct IsDiag {
+  static constexpr bool value = V >= 100 && V != 120;
+};
+
 // Fused query forms per variant (Scene::fuse bits, rtg_trace.h): every
 // sample-kernel variant except 23 (the two-pass queries, for A/B).
 template <int kVariant>
@@ -760,7 +817,11 @@ template <int S, bool kLds, int kVariant, bool kBvh, bool kList, bool kMasks>
 __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
   constexpr int kThreads = SampleThreads<kVariant>::value;
   typedef typename std::conditional<kLds, const float*, cfloat_p>::type MatPtr;
-  DevScene<MatPtr, (kVariant >= 100), kThreads, kBvh, FuseOf<kVariant>::value, kMasks> sc;
+  constexpr bool kCount = IsCount<kVariant>::value;
+  DevScene<MatPtr, IsDiag<kVariant>::value, kThreads, kBvh, FuseOf<kVariant>::value, kMasks,
+           kCount>
+      sc;
+  sc.count_reset();
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull
@@ -771,7 +832,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
   // variant 15: the previous default (shadow rays screening every sphere)
   // variant 21: kGroupsPerWave consecutive pixel groups per wave, in turn
   constexpr int Q = (kVariant == 15) ? 2 : 4;
-  constexpr bool kDiag = kVariant >= 100;
+  constexpr bool kDiag = IsDiag<kVariant>::value;
   if constexpr (kList) {
     const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
     // variant 24: the wave recomputes its primary cull (no cull-pass masks)
@@ -788,6 +849,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
       trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(a, sc,
                                                                                  gw * K + k);
   }
+  if constexpr (kCount) sc.flush_counts(kargs()->counts);
   record_wave(a, t0, gw);
 }
 
@@ -854,6 +916,8 @@ void trace_samples_kernel_masked(const KernelArgs a) {
 //   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9,
 //     110 = the default sample kernel (0)
+//   120 the default kernel's executed-work counting build (rtg_diag_counts):
+//     same control flow, unit counters per wave (DevScene kCount)
 // The one table of valid variants and their kernel kind; anything else is
 // rejected (rtg_set_launch_opts, RTG_VARIANT) and trace_fn returns nullptr.
 // kSemantic variants change results and are only chosen through
@@ -874,6 +938,7 @@ constexpr VariantInfo kVariants[] = {
     {23, kVariantSample, false}, {24, kVariantSample, false},
     {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
     {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
+    {120, kVariantSample, false},
 };
 inline const VariantInfo* variant_info(int v) {
   for (const VariantInfo& i : kVariants)
@@ -888,7 +953,7 @@ inline const VariantInfo* variant_info(int v) {
 template <int V>
 struct CompactVariant {
   static constexpr bool value = V == 0 || V == 15 || V == 17 || V == 18 || V == 19 || V == 20 ||
-                                V == 23 || V == 24 || V == 50 || V == 110;
+                                V == 23 || V == 24 || V == 50 || V == 110 || V == 120;
 };
 // list: 0 the direct launch, 1 the compacted launch, 2 the compacted launch
 // of a scene with masks (kMasks instantiation of the default kernel).
@@ -902,6 +967,9 @@ static TraceFn trace_fn_v(bool lds, int list) {
       if constexpr (S <= 6) return trace_samples_kernel_masked<S>;
       else return trace_samples_kernel<S, false, 0, false, true, true>;
     }
+  }
+  if constexpr (V == 120) {  // the counting build of exactly that kernel
+    if (list == 2) return trace_samples_kernel<S, false, 120, false, true, true>;
   }
   if constexpr (V == 17) {
     if (list)
@@ -927,6 +995,7 @@ static TraceFn trace_fn_bvh(bool lds, int variant) {
     case 0: return trace_samples_kernel<S, false, 0, true>;
     case 50: return trace_samples_kernel<S, false, 50, true>;
     case 110: return trace_samples_kernel<S, false, 110, true>;
+    case 120: return trace_samples_kernel<S, false, 120, true>;
     case 9: return lds ? trace_kernel<S, true, 9, true> : trace_kernel<S, false, 9, true>;
     case 59: return lds ? trace_kernel<S, true, 59, true> : trace_kernel<S, false, 59, true>;
     case 100: return lds ? trace_kernel<S, true, 100, true> : trace_kernel<S, false, 100, true>;
@@ -942,6 +1011,7 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh, int list) {
   switch (variant) {
     case 100: return trace_fn_v<S, 100>(lds, list);
     case 110: return trace_fn_v<S, 110>(lds, list);
+    case 120: return trace_fn_v<S, 120>(lds, list);
     case 18: return trace_fn_v<S, 18>(lds, list);
     case 19: return trace_fn_v<S, 19>(lds, list);
     case 20: return trace_fn_v<S, 20>(lds, list);

@@ -54,11 +54,27 @@ EXPORTED = [
     "rtg_last_error", "rtg_abi_version", "rtg_device_count", "rtg_device_info",
     "rtg_render", "rtg_context_create", "rtg_context_destroy", "rtg_context_set_scene",
     "rtg_shard_rows", "rtg_shard_global_row", "rtg_render_device", "rtg_render_rows_device",
-    "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read", "rtg_diag_timeline",
+    "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read", "rtg_diag_timeline", "rtg_diag_counts",
+    "rtg_context_scene_stats",
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate", "rtg_assemble_shards_device",
     "rtg_render_multi", "rtg_scene_load", "rtg_scene_save", "rtg_context_set_semantics",
     "rtg_multi_create", "rtg_multi_set_scene", "rtg_multi_render", "rtg_multi_destroy",
+]
+
+
+# Counter slots of the traversal (rtg_trace.h kCnt* then the kU* executed-work
+# units), the order of rtg_diag_counts / hostsim_counts.
+UNIT_NAMES = [
+    "samples", "primQ", "primSel", "primCand", "enterQ", "enterOK", "fullQ", "fullCand",
+    "shadowQ", "shadowSel", "shadowCand", "containMasked", "containSel", "containFull",
+    "refraction", "reflPush", "bvhNodeTests", "bvhSphereTests", "coneQ", "coneSel",
+    "bvhShadowQ", "bvhShadowNodeTests", "bvhShadowSphereTests",
+    "U.query", "U.primIter", "U.primExact", "U.selIter", "U.selExact", "U.shdIter",
+    "U.shdExact", "U.enterHead", "U.enterIter", "U.enterExact", "U.fullGroup", "U.fullExact",
+    "U.bvhNode", "U.bvhSlot", "U.bvhExact", "U.contIter", "U.cont4", "U.contBvhNode", "U.cone",
+    "U.maskIter", "U.node", "U.shade", "U.light", "U.shadow", "U.lit", "U.refr", "U.refrLeaf",
+    "U.push", "U.descend", "U.unwind", "U.sample",
 ]
 
 
@@ -95,6 +111,8 @@ def lib() -> ctypes.CDLL:
         L.rtg_context_set_semantics.argtypes = [vp, i]
         L.rtg_diag_read.argtypes = [vp, vp, i]
         L.rtg_diag_timeline.argtypes = [vp, vp, sz, vp]
+        L.rtg_diag_counts.argtypes = [vp, vp, i, i]
+        L.rtg_context_scene_stats.argtypes = [vp, vp]
         L.rtg_max_colour.argtypes = [vp, sz]
         L.rtg_max_colour.restype = f
         L.rtg_max_colour_device.argtypes = [vp, vp, sz, vp, vp]
@@ -333,6 +351,14 @@ class Context:
                                            _ptr(self._lgt), len(self._lgt)),
                "rtg_context_set_scene")
 
+    def scene_stats(self):
+        """{prep_ms, upload_ms, device_bytes, bvh_nodes} of the last set_scene."""
+        out = (ctypes.c_double * 4)()
+        _check(lib().rtg_context_scene_stats(self._h, ctypes.cast(out, ctypes.c_void_p)),
+               "rtg_context_scene_stats")
+        return {"prep_ms": out[0], "upload_ms": out[1], "device_bytes": int(out[2]),
+                "bvh_nodes": int(out[3])}
+
     LAUNCH_TIMELINE = 1  # RTG_LAUNCH_TIMELINE
     SEMANTICS_CPU, SEMANTICS_OPENCL = 0, 1  # RTG_SEMANTICS_*
 
@@ -351,6 +377,19 @@ class Context:
         _check(lib().rtg_diag_read(self._h, ctypes.cast(out, ctypes.c_void_p), int(reset)),
                "rtg_diag_read")
         return [int(v) for v in out]
+
+    def diag_counts(self, reset: bool = True):
+        """Executed-work unit counters of the counting build (variant 120):
+        (wave-level, lane-level) arrays indexed by UNIT_NAMES."""
+        n = lib().rtg_diag_counts(self._h, None, 0, 0)
+        if n < 0:
+            _check(n, "rtg_diag_counts")
+        out = (ctypes.c_ulonglong * n)()
+        rc = lib().rtg_diag_counts(self._h, ctypes.cast(out, ctypes.c_void_p), n, int(reset))
+        if rc < 0:
+            _check(rc, "rtg_diag_counts")
+        v = np.array(out[:], np.int64)
+        return v[:n // 2], v[n // 2:]
 
     def diag_timeline(self, cap: int = 1 << 20) -> np.ndarray:
         """Per-wave records {start, end, HW_ID, XCC_ID} of the last timeline-variant launch."""

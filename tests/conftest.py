@@ -22,6 +22,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "raytracer-gamma_amd")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 BUILD = os.path.join(ROOT, "tests", "_build")
+# RTG_ASAN=1: load the AddressSanitizer/UBSan builds of the CPU checkers
+# (tests/asan/Makefile; tests/test_sanitizers.py runs the suite that way).
+ASAN = os.environ.get("RTG_ASAN") == "1"
+ASAN_BUILD = os.path.join(BUILD, "asan")
 sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 
@@ -47,7 +51,9 @@ class Oracle:
 
     def __init__(self):
         path = os.path.join(ROOT, "oracle", "build", "librtg_oracle.so")
-        if not os.path.exists(path):
+        if ASAN:
+            path = os.path.join(ASAN_BUILD, "librtg_oracle.so")
+        elif not os.path.exists(path):
             _make(os.path.join(ROOT, "oracle"), "build/librtg_oracle.so")
         self.lib = ctypes.CDLL(path)
         self.lib.oracle_max_colour.restype = ctypes.c_float

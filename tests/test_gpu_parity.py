@@ -90,6 +90,37 @@ def test_c5_sampled_rows(R, golden):
     assert bits_equal(got, want), first_mismatch(got, want)
 
 
+def test_c5_wide_sample(R, golden, torch_cuda):
+    """C5 against the widened reference fixture (tests/golden/make_c5_wide.py):
+    85 full-width rows (every 32nd, the centre band 1072..1087, the last) and
+    100,000 seeded random pixels of the whole frame, from one full-frame
+    render of the default (BVH) kernel."""
+    torch = torch_cuda
+    c = golden["configs"]["c5"]
+    wide = c["wide"]
+    z = np.load(os.path.join(GOLDEN, wide["file"]))  # allow_pickle=False (default)
+    rows, want_rows, gids, want_px = z["rows"], z["rows_fb"], z["gids"], z["pixels"]
+    assert len(rows) == wide["rows"] and len(gids) == wide["pixels"]
+    assert canon_md5(want_rows) == wide["rows_md5"] and canon_md5(want_px) == wide["pixels_md5"]
+    sph, lg = load_scene("c5", c["spheres"], c["lights"])
+    W, H = c["W"], c["H"]
+    ctx = R.Context(0)
+    ctx.set_scene(sph, lg)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    ctx.render_device(W, H, out.data_ptr(), stack_size=c["stack_size"],
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    fb = out.cpu().numpy()
+    ctx.close()
+    got_rows = fb[rows.astype(np.int64)]
+    assert bits_equal(got_rows, want_rows), first_mismatch(got_rows, want_rows)
+    got_px = fb.reshape(-1, 3)[gids.astype(np.int64)]
+    assert bits_equal(got_px, want_px), first_mismatch(got_px, want_px)
+    # the old 5-row fixture agrees with the same frame
+    old = load_f32(os.path.join(GOLDEN, "c5.rows.f32"), (len(c["rows"]["rows"]), W, 3))
+    assert bits_equal(fb[c["rows"]["rows"]], old)
+
+
 def test_random_scenes_vs_oracle(R, oracle):
     rng = np.random.default_rng(2026)
     for trial in range(24):
@@ -256,12 +287,19 @@ def test_errors_are_returned_not_fatal(R):
         R.render(sph, lg, 8, 8, device=64)
     with pytest.raises(R.RtgError):
         R.render_rows(sph, lg, 8, 8, [8])
+    # scenes of RTG_MAX_SPHERES (2^23) spheres or more are rejected before the
+    # sphere array is read (the kernel's 23-bit index fields, 32-bit offsets)
+    ctx = R.Context(0)
+    one = np.zeros(1, R.SPHERE_DTYPE)
+    rc = R.lib().rtg_context_set_scene(ctx._h, ctypes.c_void_p(one.ctypes.data), 1 << 23, None, 0)
+    assert rc == -1 and b"spheres" in R.lib().rtg_last_error()
+    ctx.close()
     # still usable afterwards
     fb = R.render(sph, lg, 8, 8)
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 100, 108, 110])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 100, 108, 110, 120])
 def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
     """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
     torch = torch_cuda
@@ -279,6 +317,47 @@ def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert bits_equal(got, want), (name, variant, first_mismatch(got, want))
+    ctx.close()
+
+
+def test_counting_build(R, golden, torch_cuda):
+    """The executed-work counting build (variant 120, rtg_diag_counts): the
+    same frame bit for bit, and its lane-level counts of the per-lane
+    algorithm units equal the host build's (tests/golden/unit_counts.json);
+    wave-level counts bound lane-level ones (at most 64 lanes per wave)."""
+    import json
+    torch = torch_cuda
+    fix = json.load(open(os.path.join(GOLDEN, "unit_counts.json")))
+    ctx = R.Context(0)
+    ctx.set_variant(120)
+    for name, want in fix["frames"].items():
+        c = golden["configs"][name]
+        sph, lg = load_scene(name, c["spheres"], c["lights"])
+        sw, sh = c["small"]["W"], c["small"]["H"]
+        ctx.set_scene(sph, lg)
+        ctx.diag_counts(reset=True)
+        out = torch.empty((sh, sw, 3), dtype=torch.float32, device="cuda")
+        ctx.render_device(sw, sh, out.data_ptr(), stack_size=c["stack_size"],
+                          stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ref = load_f32(os.path.join(GOLDEN, f"{name}.small.f32"), (sh, sw, 3))
+        assert bits_equal(out.cpu().numpy(), ref), name
+        wv, lv = ctx.diag_counts(reset=True)
+        got = {u: int(lv[R.UNIT_NAMES.index(u)]) for u in fix["units"]}
+        assert got == want, (name, got, want)
+        assert (wv <= lv).all() and (lv <= 64 * wv).all(), name
+        k = R.UNIT_NAMES.index("U.sample")
+        assert 0 < lv[k] <= sw * sh * 9 and wv[k] > 0, name
+    # a BVH scene (C5, n > 64) runs its own counting instantiation
+    c = golden["configs"]["c5"]
+    sph, lg = load_scene("c5", c["spheres"], c["lights"])
+    ctx.set_scene(sph, lg)
+    out = torch.empty((54, 96, 3), dtype=torch.float32, device="cuda")
+    ctx.render_device(96, 54, out.data_ptr(), stack_size=c["stack_size"])
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), load_f32(os.path.join(GOLDEN, "c5.small.f32"), (54, 96, 3)))
+    wv, lv = ctx.diag_counts(reset=True)
+    assert wv[R.UNIT_NAMES.index("U.bvhNode")] > 0 and wv[R.UNIT_NAMES.index("U.bvhSlot")] > 0
     ctx.close()
 
 

@@ -17,7 +17,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import (BUILD, GOLDEN, P, ROOT, bits_equal, canon_md5, first_mismatch,
+from conftest import (ASAN, ASAN_BUILD, BUILD, GOLDEN, P, ROOT, bits_equal, canon_md5, first_mismatch,
                       load_f32, load_scene, md5, random_scene)
 
 REF_DIR = os.path.join(ROOT, "oracle", "_ref")
@@ -118,6 +118,8 @@ def test_reference_struct_layout(rtg):
 @pytest.fixture(scope="session")
 def hostsim():
     """Host build of the kernel's traversal (rtg_trace.h), test-only."""
+    if ASAN:  # tests/asan/Makefile build (tests/test_sanitizers.py)
+        return ctypes.CDLL(os.path.join(ASAN_BUILD, "libhostsim.so"))
     os.makedirs(BUILD, exist_ok=True)
     so = os.path.join(BUILD, "libhostsim.so")
     src = os.path.join(ROOT, "tests", "hostsim", "hostsim.cpp")
@@ -394,3 +396,37 @@ def test_cone_masks_are_conservative(hostsim):
             ctypes.byref(tested))
     assert bad == 0, bad
     assert tested.value > 200_000, tested.value
+
+
+def test_kernel_traversal_c5_wide_rows(hostsim, golden):
+    """The kernel's BVH traversal (host build) on C5 (1024 spheres, depth 7)
+    against the widened reference fixture: two centre-band rows, where most
+    rays enter the sphere cluster, and the random pixels that fall in them."""
+    c = golden["configs"]["c5"]
+    z = np.load(os.path.join(GOLDEN, c["wide"]["file"]))
+    rows = list(z["rows"])
+    sph, lg = load_scene("c5", c["spheres"], c["lights"])
+    hostsim.hostsim_set_variant(0)
+    pick = [1080, 1084]
+    got = _hostsim_render(hostsim, sph, lg, c["W"], c["H"], c["stack_size"], rows=pick)
+    for k, r in enumerate(pick):
+        want = z["rows_fb"][rows.index(r)]
+        assert bits_equal(got[k], want), (r, first_mismatch(got[k], want))
+    gids = z["gids"].astype(np.int64)
+    sel = np.isin(gids // c["W"], pick)
+    assert sel.sum() > 50
+    flat = {r: got[k] for k, r in enumerate(pick)}
+    px = np.stack([flat[g // c["W"]][g % c["W"]] for g in gids[sel]])
+    assert bits_equal(px, z["pixels"][sel])
+
+
+def test_unit_counts_fixture_matches_hostsim(hostsim, golden):
+    """tests/golden/unit_counts.json (the per-lane unit counts the GPU test
+    holds the device counting build to) is the current traversal's."""
+    import json
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_unit_counts as muc
+    want = json.load(open(os.path.join(GOLDEN, "unit_counts.json")))
+    assert want["units"] == muc.UNITS
+    assert muc.hostsim_counts(hostsim, golden) == want["frames"]

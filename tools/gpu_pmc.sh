@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out
 TAG=${TAG:-r01}
-ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-work-count --no-e2e"}
 mkdir -p $OUT/pmc_$TAG
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $OUT/pmc_$TAG/counters_list.txt 2>&1 || true

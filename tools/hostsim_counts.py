@@ -14,10 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from conftest import BUILD, GOLDEN, P, load_scene  # noqa: E402
 
-NAMES = ["samples", "primQ", "primSel", "primCand", "enterQ", "enterOK", "fullQ", "fullCand",
-         "shadowQ", "shadowSel", "shadowCand", "containMasked", "containSel", "containFull",
-         "refraction", "reflPush", "bvhNodeTests", "bvhSphereTests", "coneQ", "coneSel",
-         "bvhShadowQ", "bvhShadowNodeTests", "bvhShadowSphereTests"]
+sys.path.insert(0, os.path.join(ROOT, "raytracer-gamma_amd"))
+from rtg_amd import UNIT_NAMES as NAMES  # noqa: E402
 
 
 def main():
