@@ -86,8 +86,8 @@ def cpu_baseline(name, sph, lg, W, H, S, budget_s):
     on one host thread (the reference's main.cpp:404 loop is single-threaded)
     and on all host threads; falls back to the C restatement
     (rows) if the reference build is absent.  Each leg gets half of
-    `budget_s`: a 256-pixel calibration run sizes the sample to fill it (C5's
-    pixels cost ~1000x C3's).  The multi-threaded figure is the baseline; the
+    `budget_s`: the sample grows until one run fills half of it (C5's pixels
+    cost ~1000x C3's).  The multi-threaded figure is the baseline; the
     frame time is extrapolated from the sample."""
     ref = os.path.join(ROOT, "oracle", "_ref", f"librtgref_S{S}.so")
     port = os.path.join(ROOT, "oracle", "build", "librtg_oracle.so")
@@ -114,9 +114,14 @@ def cpu_baseline(name, sph, lg, W, H, S, budget_s):
         return time.perf_counter() - t0, gids, out.reshape(-1, 3)
 
     def leg(threads, budget):
-        t_cal, _, _ = run(256, threads)
-        n = int(min(W * H, max(256, 256 * budget / max(t_cal, 1e-6))))
-        t, gids, out = run(n, threads)
+        # grow the sample until one run fills at least half the budget (a
+        # short run on many threads is dominated by start-up and tail)
+        n = 64 * threads
+        while True:
+            t, gids, out = run(n, threads)
+            if t >= 0.5 * budget or n >= W * H:
+                break
+            n = int(min(W * H, n * min(16.0, max(2.0, 0.8 * budget / max(t, 1e-6)))))
         px = len(gids)
         return {"value": round(px / t / 1e6, 5), "unit": "Mpixels/s", "cores": threads,
                 "kind": kind,

@@ -51,8 +51,8 @@ struct PackedScene {
   // the sphere masks; empty otherwise.
   std::vector<unsigned> cone;
   // BVH of scenes above kMaskMaxSpheres spheres (build_bvh): per node 4
-  // slots {x, y, z, screen radius^2} (bound_r2 for a child node, screen_r2
-  // for a sphere), 4 children (> 0 node, < 0 ~sphere index, 0 empty) and 4
+  // slots {x, y, z, w}: w = bound_r1 (R (1 + m), bound_screen) for a child
+  // node, screen_r2 (r^2, pass1_rad) for a sphere; 4 children (> 0 node, < 0 ~sphere index, 0 empty) and 4
   // {prune radius, containment radius^2}; empty for small or non-finite
   // scenes.
   std::vector<float> bvhNodes, bvhAux;
@@ -311,7 +311,7 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
 // four groups; a group of one sphere becomes a sphere slot, a larger group a child
 // node; nodes of <= 4 spheres hold sphere slots only.  Bounds are computed in
 // double about the float-rounded centre C of the group's box:
-//   R  = max |c_i - C| + |r_i|            (screen: bound_r2(R (1 + 2^-20)))
+//   R  = max |c_i - C| + |r_i|            (screen: bound_r1(R), bound_screen)
 //   RC = (max |c_i - C| + |r_i| + 1e-6) (1 + 2^-16)   (containment, RC^2 up)
 //   prune radius R (1 + 2^-7), rounded up (|r_i| (1 + 2^-7) for a sphere
 //   slot; see beyond_t in rtg_trace.h).
@@ -460,7 +460,7 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
       } else {
         double R, RC;
         bound(a, b, C, R, RC);
-        w = bound_r2(R * (1.0 + 0x1p-20));
+        w = RTG_BVH_OLD_SCREEN ? bound_r2(R * (1.0 + 0x1p-20)) : bound_r1(R);
         cr = round_up_f(RC * RC);
         rp = round_up_f(R * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
         child = build(a, b, depth + 1);

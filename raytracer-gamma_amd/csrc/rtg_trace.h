@@ -223,6 +223,7 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kUDescend,     // descent to the refraction child (frame, I, o, d)
              kUUnwind,      // one unwind step (stage 1/2 colour sums)
              kUSample,      // one primary sample: ray set-up, cull hand-over, pixel sum
+             kUBvhPass,     // (diagnostic) a BVH child-node screen passes for the lane
              kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
@@ -275,14 +276,24 @@ struct Frame {
 // property over 1e9 operand pairs (incl. subnormal numerators and values at
 // both thresholds) for den in [2^-60, 2^60].  Outside that range the correctly
 // rounded division is used.
-// Slack of the BVH node screens (bound_r2, rtg_scene_pack.h build_bvh).
+// BVH node screens (bound_screen / bound_r1, rtg_scene_pack.h build_bvh):
+// the line-distance margin m of a node bound, and the relative slack of the
+// screen's float evaluation.  RTG_BVH_OLD_SCREEN (A/B builds only): the
+// round-2 radicand screen with slack K_B = 2^-7 relative to |p|^2 + R^2.
+#ifndef RTG_BVH_OLD_SCREEN
+#define RTG_BVH_OLD_SCREEN 0
+#endif
 constexpr float kBoundK = 0x1p-7f;
+constexpr double kBoundM = 0x1p-8;               // m
+constexpr float kBoundMK = 0x1.00004p-8f;        // m (1 + 2^-18)
+constexpr float kBoundSlack = 0x1p-18f;
 
 struct RayQ {
   V3 o, d;
   float a4, den, y;
   float ap;       // pass-1 screen: a (1 - K), K = 2^-16 (pass1_rad)
-  float apB;      // BVH bound screen: a (1 - K_B), K_B = kBoundK (bound_r2)
+  float apB;      // BVH bound screen (RTG_BVH_OLD_SCREEN): a (1 - K_B)
+  float bL, bH;   // BVH bound screen: a (1 -+ kBoundSlack)
   bool fast;
 };
 
@@ -295,6 +306,8 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.den = 2.0f * a;
   q.ap = a * (1.0f - 0x1p-16f);
   q.apB = a * (1.0f - kBoundK);
+  q.bL = a * (1.0f - kBoundSlack);
+  q.bH = a * (1.0f + kBoundSlack);
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
   // y is used only when q.fast (quot, quot_k<true>); den is then in
   // [2^-60, 2^60], inside rcp_fast's range, so no range check is needed.
@@ -1056,13 +1069,55 @@ inline float screen_r2(float r2) {
 //  * shadow (raytracer.h:272-309) = does ANY accepted root block;
 //  * container (raytracer.h:245-270) = the minimum index whose containment
 //    test passes.
-// A node bound (C, R) holds every member sphere (R >= |c_i - C| + |r_i|); its
-// screen is pass1_rad's with slack K_B = kBoundK instead of K: a line the
-// reference accepts for member i passes within R + sqrt(E/a) of C, E ~ 10 eps
-// a (|p_i|^2 + r_i^2) being the reference radicand's rounding error, so the
-// bound's true radicand/4 is >= -2 sqrt(30 eps) a (|p_B|^2 + R^2) ~ -2^-8.5
-// a (...), which K_B = 2^-7 covers with room for the screen's own rounding
-// (tests/test_oracle.py::test_bvh_bound_screen_is_a_superset).
+// A node bound (C, R) holds every member sphere (R >= |c_i - C| + |r_i|).
+// Which lines can the reference accept for member i?  Its radicand
+// (raytracer.h:95-104) carries a rounding error E <= ~60 eps a (|p_i|^2 +
+// r_i^2) (p_i = o - c_i: the subtraction, two dot products, the products and
+// the difference), so a computed radicand >= 0 implies a (r_i^2 - d_i^2) >=
+// -E/4 for the distance d_i from c_i to the line, i.e. d_i^2 <= r_i^2 + 15
+// eps (|p_i|^2 + r_i^2): d_i <= r_i (1 + 4 sqrt(eps)) + sqrt(15 eps) |p_i|
+// (sqrt(15 eps) ~ 9.5e-4; tests/test_oracle.py measures misses of up to
+// ~7e-4 |p| accepted).  With |p_i| <= |p_B| + R (p_B = o - C) the line passes
+// within
+//     R_m = R + m (|p_B| + R),   m = 2^-8 (four times that bound)
+// of C.  bound_screen tests exactly that, as a radicand: x^2 - a |p_B|^2 +
+// a R_m^2 >= 0 (x = d.p_B), with R_m from one hardware square root, R (1 + m)
+// rounded up on the host (bound_r1) and m inflated by 2^-18 (the square
+// root's and the fused step's rounding), and the two a-terms scaled by
+// 1 -+ 2^-18 to cover the float evaluation's own error (< 20 eps a (|p_B|^2
+// + R_m^2)), so every line within R_m of C passes.  The slack is linear in
+// |p_B|: a node 40 units away keeps its radius within ~4 %, where the
+// round-2 screen (slack K_B a (|p_B|^2 + R^2), K_B = 2^-7, pass1_bound below)
+// let the bound grow by K_B |p_B|^2 / (2 R), several radii for a small far
+// node.  (tests/test_oracle.py::test_bvh_bounds_are_conservative checks it
+// on adversarial near-tangent and far, tiny spheres.)
+RTG_HD float sqrt_hw(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sqrtf(x);  // v_sqrt_f32, within 1 ulp
+#else
+  return sqrtf(x);
+#endif
+}
+RTG_HD float bound_screen_p(const RayQ& q, float xd, float p2, float R1) {
+  const float Rm = fmaf(sqrt_hw(p2), kBoundMK, R1);
+  return fmaf(xd, xd, fmaf(-q.bL, p2, q.bH * (Rm * Rm)));
+}
+RTG_HD float bound_screen(const RayQ& q, V3 c, float R1) {
+  const V3 p = vsub(q.o, c);
+  const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+  const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
+  return bound_screen_p(q, x, p2, R1);
+}
+// R (1 + m) (1 + 2^-20) rounded up to float, R given in double.
+inline float bound_r1(double R) {
+  const double v = R * (1.0 + kBoundM) * (1.0 + 0x1p-20);
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, __builtin_inff());
+  return f;
+}
+
+// Round-2 node screen (RTG_BVH_OLD_SCREEN A/B builds): pass1_rad's with slack
+// K_B = kBoundK instead of K, i.e. K_B a (|p_B|^2 + R^2).
 RTG_HD float pass1_bound(const RayQ& q, V3 c, float rsB) {
   const V3 p = vsub(q.o, c);
   const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
@@ -1178,8 +1233,12 @@ RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool activ
     const bool near = !beyond(p2, rp[k], reach);
     if (x > 0) {
       sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
-      const float v = fmaf(xd, xd, fmaf(-q.apB, p2 - w[k], 0x1p-100f));  // pass1_bound
-      if (sc.any(active && near && !(v < 0.f))) {
+      const float v = RTG_BVH_OLD_SCREEN
+                          ? fmaf(xd, xd, fmaf(-q.apB, p2 - w[k], 0x1p-100f))  // pass1_bound
+                          : bound_screen_p(q, xd, p2, w[k]);
+      const bool pass = active && near && !(v < 0.f);
+      if (pass) sc.count(kUBvhPass, 1);
+      if (sc.any(pass)) {
         pc[k] = x;
         pk[k] = sc.first_lane(p2);
       }

@@ -74,7 +74,7 @@ UNIT_NAMES = [
     "U.shdExact", "U.enterHead", "U.enterIter", "U.enterExact", "U.fullGroup", "U.fullExact",
     "U.bvhNode", "U.bvhSlot", "U.bvhExact", "U.contIter", "U.cont4", "U.contBvhNode", "U.cone",
     "U.maskIter", "U.node", "U.shade", "U.light", "U.shadow", "U.lit", "U.refr", "U.refrLeaf",
-    "U.push", "U.descend", "U.unwind", "U.sample",
+    "U.push", "U.descend", "U.unwind", "U.sample", "U.bvhPass",
 ]
 
 

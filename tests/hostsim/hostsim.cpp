@@ -140,6 +140,8 @@ struct HostScene {
 
 int g_variant = 0;
 bool g_useBvh = true;
+bool g_oldBoundScreen = false;  // hostsim_bvh_bound_check: the round-2 node screen
+double g_boundM = 0.0;          // hostsim_bvh_bound_check: margin m probe (0: kBoundM)
 
 template <int S>
 void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, float* out) {
@@ -215,6 +217,8 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
+extern "C" void hostsim_old_bound_screen(int on) { g_oldBoundScreen = on != 0; }
+extern "C" void hostsim_bound_margin(double m) { g_boundM = m; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
 // the renders since the last reset (diagnostic; single-lane semantics, so the
 // wave unions of the GPU are per-sample masks here).
@@ -666,8 +670,24 @@ extern "C" long hostsim_bvh_bound_check(long trials, unsigned long long seed, lo
                               (float)(c.z + off * oz / ol));
     const double cx = (double)c.x - C.x, cy = (double)c.y - C.y, cz = (double)c.z - C.z;
     const double R = sqrt(cx * cx + cy * cy + cz * cz) + fabs((double)r);
-    const float w = rtg::bound_r2(R * (1.0 + 0x1p-20));
-    if (rtg::pass1_bound(q, C, w) < 0.f) ++badS;
+    if (g_oldBoundScreen) {
+      const float w = rtg::bound_r2(R * (1.0 + 0x1p-20));
+      if (rtg::pass1_bound(q, C, w) < 0.f) ++badS;
+    } else {
+      // the kernel's screen with the device's square root, which may be 1 ulp
+      // low (the host's sqrtf rounds correctly): test with s (1 - 2^-23)
+      const rtg::V3 pB = rtg::vsub(o, C);
+      const float x = fmaf(d.x, pB.x, fmaf(d.y, pB.y, d.z * pB.z));
+      const float p2 = fmaf(pB.x, pB.x, fmaf(pB.y, pB.y, pB.z * pB.z));
+      float R1 = rtg::bound_r1(R), mK = rtg::kBoundMK;
+      if (g_boundM > 0.0) {  // margin probe: the same screen with another m
+        R1 = rtg::round_up_f(R * (1.0 + g_boundM) * (1.0 + 0x1p-20));
+        mK = (float)(g_boundM * (1.0 + 0x1p-18));
+      }
+      const float Rm = fmaf(sqrtf(p2) * (1.0f - 0x1p-23f), mK, R1);
+      if (fmaf(x, x, fmaf(-q.bL, p2, q.bH * (Rm * Rm))) < 0.f) ++badS;
+      else if (g_boundM == 0.0 && rtg::bound_screen(q, C, R1) < 0.f) ++badS;
+    }
     // root distance: reach = 0.999999 t |d| must not prune the sphere itself
     const float rp = rtg::round_up_f(fabs((double)r) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
     const rtg::V3 p = rtg::vsub(o, c);

@@ -345,7 +345,8 @@ def test_counting_build(R, golden, torch_cuda):
         wv, lv = ctx.diag_counts(reset=True)
         got = {u: int(lv[R.UNIT_NAMES.index(u)]) for u in fix["units"]}
         assert got == want, (name, got, want)
-        assert (wv <= lv).all() and (lv <= 64 * wv).all(), name
+        u = np.array([nm.startswith("U.") for nm in R.UNIT_NAMES])  # 1 per lane and execution
+        assert (wv[u] <= lv[u]).all() and (lv[u] <= 64 * wv[u]).all(), name
         k = R.UNIT_NAMES.index("U.sample")
         assert 0 < lv[k] <= sw * sh * 9 and wv[k] > 0, name
     # a BVH scene (C5, n > 64) runs its own counting instantiation

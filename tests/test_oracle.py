@@ -346,19 +346,36 @@ def test_overlap_masks_bound_containment(hostsim):
 
 
 def test_bvh_bounds_are_conservative(hostsim):
-    """BVH node screens (pass1_bound, slack K_B = 2^-7) keep every sphere the
-    reference's root test accepts, and the distance prune (beyond) never drops
-    an accepted root, over 3M adversarial near-tangent / far / on-surface
-    ray-sphere pairs at scales 1e-3..1e3 (rtg_trace.h closest_bvh).  The
-    tiny-far-sphere cases (lines the reference accepts although they miss by
-    up to ~7e-4 |p|) need K_B >= ~2^-11.2: at 2^-12 this test fails."""
+    """BVH node screens (bound_screen: every line within R + m (|p_B| + R) of
+    the node centre passes, m = 2^-8) keep every sphere the reference's root
+    test accepts, and the distance prune (beyond) never drops an accepted
+    root, over 3M adversarial near-tangent / far / on-surface ray-sphere pairs
+    at scales 1e-3..1e3 (rtg_trace.h closest_bvh).  The tiny-far-sphere cases
+    (lines the reference accepts although they miss by up to ~7e-4 |p|) need
+    m >= ~2^-10.5: at m = 2^-12 the same check finds misses.  The round-2
+    screen (pass1_bound, K_B = 2^-7; RTG_BVH_OLD_SCREEN builds) passes too."""
     f = hostsim.hostsim_bvh_bound_check
     f.restype = ctypes.c_long
-    acc, bad_screen = ctypes.c_long(0), ctypes.c_long(0)
-    bad = f(ctypes.c_long(3_000_000), ctypes.c_ulonglong(2026), ctypes.byref(acc),
-            ctypes.byref(bad_screen))
-    assert bad == 0 and bad_screen.value == 0, (bad, bad_screen.value)
-    assert acc.value > 500_000, acc.value
+    hostsim.hostsim_bound_margin.argtypes = [ctypes.c_double]
+
+    def run(trials, seed):
+        acc, bad_screen = ctypes.c_long(0), ctypes.c_long(0)
+        bad = f(ctypes.c_long(trials), ctypes.c_ulonglong(seed), ctypes.byref(acc),
+                ctypes.byref(bad_screen))
+        return bad, bad_screen.value, acc.value
+
+    bad, bad_screen, acc = run(3_000_000, 2026)
+    assert bad == 0 and bad_screen == 0, (bad, bad_screen)
+    assert acc > 500_000, acc
+    try:
+        hostsim.hostsim_bound_margin(2.0 ** -12)
+        assert run(1_000_000, 2027)[1] > 0  # the check has teeth
+        hostsim.hostsim_bound_margin(0.0)
+        hostsim.hostsim_old_bound_screen(1)
+        assert run(1_000_000, 2028)[:2] == (0, 0)
+    finally:
+        hostsim.hostsim_bound_margin(0.0)
+        hostsim.hostsim_old_bound_screen(0)
 
 
 def test_kernel_traversal_bvh_random_scenes(hostsim, oracle):

@@ -16,7 +16,8 @@ done
 shift $((OPTIND - 1))
 for r in $(seq "$N"); do
   for L in "$@"; do
-    RTG_LIB=$L timeout -k 10 200 python bench.py --config "$C" --steps 10 --warmup 2 --no-cpu-baseline 2>/dev/null \
-      | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('$C', '$(basename "$L")', d['kernel_ms'], d['parity'].get('fb_md5_match'), flush=True)" || exit 1
+    RTG_LIB=$L timeout -k 10 200 python bench.py --config "$C" --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline \
+        --no-work-count --no-e2e 2>/dev/null \
+      | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('$C', '$(basename "$L")', d['kernel_ms'], d['parity'].get('bit_exact'), flush=True)" || exit 1
   done
 done
