@@ -232,9 +232,7 @@ struct rtg_context {
   unsigned* smask = nullptr;  // shadow masks (null when the scene has none)
   unsigned* cone = nullptr;   // secondary-ray cone masks (null when none)
   float* prim = nullptr;      // primary-cull sphere constants
-  float* bvhNodes = nullptr;  // BVH (null when the scene has none)
-  float* bvhAux = nullptr;
-  int* bvhChild = nullptr;
+  float* bvhNodes = nullptr;  // BVH node records (null when the scene has none)
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   unsigned long long* counts = nullptr;  // unit counters of the counting build (variant 120)
@@ -276,12 +274,8 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->prim);
   c->prim = nullptr;
   (void)hipFree(c->bvhNodes);
-  (void)hipFree(c->bvhAux);
-  (void)hipFree(c->bvhChild);
   c->smask = nullptr;
   c->bvhNodes = nullptr;
-  c->bvhAux = nullptr;
-  c->bvhChild = nullptr;
   c->geom = nullptr;
   c->crad2 = nullptr;
   c->mats = nullptr;
@@ -540,19 +534,13 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->cone, ps.cone.data(), ps.cone.size() * sizeof(unsigned),
                       hipMemcpyHostToDevice));
   }
-  if (!ps.bvhChild.empty()) {
-    if (hipMalloc(&ctx->bvhNodes, ps.bvhNodes.size() * sizeof(float)) != hipSuccess ||
-        hipMalloc(&ctx->bvhAux, ps.bvhAux.size() * sizeof(float)) != hipSuccess ||
-        hipMalloc(&ctx->bvhChild, ps.bvhChild.size() * sizeof(int)) != hipSuccess) {
+  if (!ps.bvhNodes.empty()) {
+    if (hipMalloc(&ctx->bvhNodes, ps.bvhNodes.size() * sizeof(float)) != hipSuccess) {
       free_scene(ctx);
       rtg_set_error("hipMalloc failed for the BVH");
       return RTG_ERR_NOMEM;
     }
     HIP_TRY(hipMemcpy(ctx->bvhNodes, ps.bvhNodes.data(), ps.bvhNodes.size() * sizeof(float),
-                      hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ctx->bvhAux, ps.bvhAux.data(), ps.bvhAux.size() * sizeof(float),
-                      hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ctx->bvhChild, ps.bvhChild.data(), ps.bvhChild.size() * sizeof(int),
                       hipMemcpyHostToDevice));
   }
   ctx->n = sphNum;
@@ -563,11 +551,10 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   ctx->sceneStats[0] = std::chrono::duration<double, std::milli>(tUp - tPack).count();
   ctx->sceneStats[1] = std::chrono::duration<double, std::milli>(tEnd - tUp).count();
   ctx->sceneStats[2] = (double)((ps.geom.size() + ps.crad2.size() + ps.mats.size() +
-                                 ps.lights.size() + ps.prim.size() + ps.bvhNodes.size() +
-                                 ps.bvhAux.size()) * sizeof(float) +
-                                (ps.smask.size() + ps.cone.size()) * sizeof(unsigned) +
-                                ps.bvhChild.size() * sizeof(int));
-  ctx->sceneStats[3] = (double)(ps.bvhChild.size() / 4);
+                                 ps.lights.size() + ps.prim.size() + ps.bvhNodes.size()) *
+                                    sizeof(float) +
+                                (ps.smask.size() + ps.cone.size()) * sizeof(unsigned));
+  ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / kBvhWords);
   return RTG_OK;
 }
 
@@ -634,8 +621,6 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.cone = ctx->cone;
   a.prim = ctx->prim;
   a.bvhNodes = ctx->bvhNodes;
-  a.bvhAux = ctx->bvhAux;
-  a.bvhChild = ctx->bvhChild;
   a.n = ctx->n;
   a.m = ctx->m;
   a.n4 = ctx->n4;

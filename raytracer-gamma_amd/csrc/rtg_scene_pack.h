@@ -50,13 +50,10 @@ struct PackedScene {
   // Secondary-ray cone masks (cone_masks): n x kConeTiers x kConeCells x {lo, hi}, with
   // the sphere masks; empty otherwise.
   std::vector<unsigned> cone;
-  // BVH of scenes above kMaskMaxSpheres spheres (build_bvh): per node 4
-  // slots {x, y, z, w}: w = bound_r1 (R (1 + m), bound_screen) for a child
-  // node, screen_r2 (r^2, pass1_rad) for a sphere; 4 children (> 0 node, < 0 ~sphere index, 0 empty) and 4
-  // {prune radius, containment radius^2}; empty for small or non-finite
-  // scenes.
-  std::vector<float> bvhNodes, bvhAux;
-  std::vector<int> bvhChild;
+  // BVH of scenes above kMaskMaxSpheres spheres (build_bvh): one 128-byte
+  // record of kBvhWords words per node (rtg_trace.h BvhRec, loaded with two
+  // 64-byte scalar loads); empty for small or non-finite scenes.
+  std::vector<float> bvhNodes;
   unsigned n = 0, m = 0;
   unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records + the fused part
 };
@@ -324,8 +321,6 @@ inline float round_up_f(double v) {
 
 inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
   ps->bvhNodes.clear();
-  ps->bvhAux.clear();
-  ps->bvhChild.clear();
   if (n <= kMaskMaxSpheres) return false;
   auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
   for (unsigned i = 0; i < n; ++i)
@@ -427,10 +422,13 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
   std::function<int(unsigned, unsigned, int)> build = [&](unsigned lo, unsigned hi,
                                                           int depth) -> int {
     maxDepth = depth > maxDepth ? depth : maxDepth;
-    const int node = (int)(ps->bvhChild.size() / 4);
-    ps->bvhNodes.resize(ps->bvhNodes.size() + 16, __builtin_nanf(""));
-    ps->bvhAux.resize(ps->bvhAux.size() + 8, -1.f);
-    ps->bvhChild.resize(ps->bvhChild.size() + 4, 0);
+    const int node = (int)(ps->bvhNodes.size() / kBvhWords);
+    ps->bvhNodes.resize(ps->bvhNodes.size() + kBvhWords, 0.f);
+    {  // empty slots: NaN geometry, aux -1, child 0, r^2 0
+      float* e = &ps->bvhNodes[(size_t)node * kBvhWords];
+      for (int k = 0; k < 16; ++k) e[k] = __builtin_nanf("");
+      for (int k = 16; k < 24; ++k) e[k] = -1.f;
+    }
     unsigned g[5];
     const unsigned cnt = hi - lo;
     if (cnt <= 4) {
@@ -447,12 +445,13 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
       const unsigned a = g[k], b = g[k + 1];
       if (a >= b) continue;
       int child;
-      float C[3], w, cr, rp;
+      float C[3], w, cr, rp, r2 = 0.f;
       if (b - a == 1) {
         const unsigned i = idx[a];
         const rtg_sphere& s = spheres[i];
         C[0] = s.pos.x; C[1] = s.pos.y; C[2] = s.pos.z;
-        w = screen_r2(s.radius * s.radius);
+        r2 = s.radius * s.radius;  // raytracer.h:100, the leaf's exact root test
+        w = screen_r2(r2);
         const float rc = s.radius + 1.0e-6f;
         cr = rc * rc;
         rp = round_up_f(fabs((double)s.radius) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
@@ -465,19 +464,18 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
         rp = round_up_f(R * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
         child = build(a, b, depth + 1);
       }
-      float* rec = &ps->bvhNodes[(size_t)node * 16 + 4 * k];
-      rec[0] = C[0]; rec[1] = C[1]; rec[2] = C[2]; rec[3] = w;
-      ps->bvhAux[(size_t)node * 8 + 2 * k] = rp;
-      ps->bvhAux[(size_t)node * 8 + 2 * k + 1] = cr;
-      ps->bvhChild[(size_t)node * 4 + k] = child;
+      float* rec = &ps->bvhNodes[(size_t)node * kBvhWords];
+      rec[4 * k + 0] = C[0]; rec[4 * k + 1] = C[1]; rec[4 * k + 2] = C[2]; rec[4 * k + 3] = w;
+      rec[16 + 2 * k] = rp;
+      rec[16 + 2 * k + 1] = cr;
+      memcpy(&rec[24 + k], &child, 4);
+      rec[28 + k] = r2;
     }
     return node;
   };
   build(0, n, 0);
   if (maxDepth > 20) {  // the wave stack holds 3 * depth + 1 <= 64 entries
     ps->bvhNodes.clear();
-    ps->bvhAux.clear();
-    ps->bvhChild.clear();
     return false;
   }
   return true;

@@ -295,6 +295,7 @@ struct RayQ {
   float apB;      // BVH bound screen (RTG_BVH_OLD_SCREEN): a (1 - K_B)
   float bL, bH;   // BVH bound screen: a (1 -+ kBoundSlack)
   bool fast;
+  bool slow;      // some active lane of the wave is not `fast` (wave-uniform)
 };
 
 RTG_HD RayQ make_query(V3 o, V3 d) {
@@ -309,21 +310,27 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.bL = a * (1.0f - kBoundSlack);
   q.bH = a * (1.0f + kBoundSlack);
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
+  q.slow = any_lane(!q.fast);
   // y is used only when q.fast (quot, quot_k<true>); den is then in
   // [2^-60, 2^60], inside rcp_fast's range, so no range check is needed.
   q.y = rcp_fast(q.den);
   return q;
 }
 
+// The Markstein quotient for every lane; lanes outside its range take the
+// division in a branch the wave skips unless one of its lanes needs it
+// (q.slow, decided once per query).
 RTG_HD float quot(float x, const RayQ& q) {
-  if (q.fast) {
-    const float q0 = x * q.y;
-    const float r0 = fmaf(-q0, q.den, x);
-    const float q1 = fmaf(r0, q.y, q0);
-    const float r1 = fmaf(-q1, q.den, x);
-    return fmaf(r1, q.y, q1);
+  const float q0 = x * q.y;
+  const float r0 = fmaf(-q0, q.den, x);
+  const float q1 = fmaf(r0, q.y, q0);
+  const float r1 = fmaf(-q1, q.den, x);
+  float r = fmaf(r1, q.y, q1);
+  if (q.slow) {
+    no_speculate();
+    if (!q.fast) r = x / q.den;
   }
-  return x / q.den;
+  return r;
 }
 
 // Per-sphere ray test, raytracer.h:81-141.  Returns the smallest root in
@@ -1184,11 +1191,28 @@ RTG_HD bool beyond(float p2, float rp, float reach) {
 // |d| rounded up (v_sqrt_f32 is within 1 ulp).
 RTG_HD float norm_up(float a) { return sqrtf(a) * (1.0f + 0x1p-20f); }
 
-// Children of a node in front-to-back order for the wave: pushes the valid
-// (child, key) pairs, keys = a lane's |p_B|^2 (wave-uniform), farthest first
-// so that the nearest is popped next.  Five compare-exchanges.
-RTG_HD void push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2, float k2,
-                        int c3, float k3) {
+// BVH node record (build_bvh, rtg_scene_pack.h): kBvhWords words, read with
+// two 64-byte scalar loads at the top of a node visit, so the four slots'
+// tests run back to back on SGPR operands (no load latency per slot).
+//   g[4k..4k+3]  slot k: centre, w (bound_r1 for a child node, screen_r2 for
+//                a sphere)
+//   aux[2k]      prune radius rp, aux[2k+1] containment radius^2
+//   ch[k]        > 0 child node, < 0 ~sphere index, 0 empty
+//   r2[k]        a sphere slot's r*r (raytracer.h:100) for the exact test
+constexpr int kBvhWords = 32;
+struct BvhRec {
+  float g[16];
+  float aux[8];
+  int ch[4];
+  float r2[4];
+};
+
+// Children of a node in front-to-back order for the wave: of the valid
+// (child, key) pairs, keys = a lane's |p_B|^2 (wave-uniform), the nearest is
+// returned (the next node: no stack round trip) and the others are pushed
+// farthest first.  Five compare-exchanges.
+RTG_HD int push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2, float k2,
+                       int c3, float k3) {
   auto cx = [](int& ca, float& ka, int& cb, float& kb) {
     if (kb > ka) {
       const int ct = ca; ca = cb; cb = ct;
@@ -1200,42 +1224,51 @@ RTG_HD void push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2
   cx(c0, k0, c2, k2);
   cx(c1, k1, c3, k3);
   cx(c1, k1, c2, k2);
-  if (c0 > 0) st.push(c0);
-  if (c1 > 0) st.push(c1);
-  if (c2 > 0) st.push(c2);
-  if (c3 > 0) st.push(c3);
+  int nxt = 0;
+  auto put = [&](int c) {
+    if (c > 0) {
+      if (nxt > 0) st.push(nxt);
+      nxt = c;
+    }
+  };
+  put(c0);
+  put(c1);
+  put(c2);
+  put(c3);
+  return nxt;
 }
 
 // One node of a ray query: bound screens and distance pruning of its four
-// slots; child nodes some active lane still needs are pushed front to back,
-// sphere slots are handed to `leaf(i, c)` for lanes that pass the screen and
-// the prune.  `active`: the lane still queries; `reach`: its pruning reach.
+// slots; child nodes some active lane still needs are ordered front to back
+// (the nearest returned, the others pushed), sphere slots are handed to
+// `leaf(i, c, r2)` for lanes that pass the screen and the prune.  `active`:
+// the lane still queries; `reach`: its pruning reach.  Returns the next node
+// (> 0) or 0.
 template <class Scene, class Leaf>
-RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active, float reach,
-                         BvhStack& st, Leaf&& leaf, bool shadowQ = false) {
-  V3 c[4];
-  float w[4], rp[4], cr[4];
-  int ch[4];
-  sc.bvh_node(nd, c, w, ch);
-  sc.bvh_aux(nd, rp, cr);
+RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active, float reach,
+                        BvhStack& st, Leaf&& leaf, bool shadowQ = false) {
+  BvhRec r;
+  sc.bvh_rec(nd, r);
   int pc[4];
   float pk[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     pc[k] = 0;
     pk[k] = 0.f;
-    const int x = ch[k];
+    const int x = r.ch[k];
     if (x == 0) continue;  // wave-uniform
     sc.count(kUBvhSlot, 1);
-    const V3 p = vsub(q.o, c[k]);
+    const V3 c = v3(r.g[4 * k], r.g[4 * k + 1], r.g[4 * k + 2]);
+    const float w = r.g[4 * k + 3];
+    const V3 p = vsub(q.o, c);
     const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-    const bool near = !beyond(p2, rp[k], reach);
+    const bool near = !beyond(p2, r.aux[2 * k], reach);
     if (x > 0) {
       sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
       const float v = RTG_BVH_OLD_SCREEN
-                          ? fmaf(xd, xd, fmaf(-q.apB, p2 - w[k], 0x1p-100f))  // pass1_bound
-                          : bound_screen_p(q, xd, p2, w[k]);
+                          ? fmaf(xd, xd, fmaf(-q.apB, p2 - w, 0x1p-100f))  // pass1_bound
+                          : bound_screen_p(q, xd, p2, w);
       const bool pass = active && near && !(v < 0.f);
       if (pass) sc.count(kUBvhPass, 1);
       if (sc.any(pass)) {
@@ -1244,11 +1277,11 @@ RTG_HD void bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool activ
       }
     } else {
       sc.count(shadowQ ? kCntBvhShadowSphereTests : kCntBvhSphereTests, 1);
-      const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - w[k], 0x1p-100f));  // pass1_rad
-      if (active && near && !(v < 0.f)) leaf((unsigned)~x);
+      const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - w, 0x1p-100f));  // pass1_rad
+      if (active && near && !(v < 0.f)) leaf((unsigned)~x, c, r.r2[k]);
     }
   }
-  push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
+  return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
 }
 
 template <class Scene>
@@ -1257,15 +1290,12 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
   int best = -1;
   const float dn = norm_up(q.den * 0.5f);
   BvhStack st(sc.bvh_stack());
-  st.push(0);
-  while (!st.empty()) {  // wave-uniform
-    const unsigned nd = (unsigned)st.pop();
+  unsigned nd = 0;  // the root
+  for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
-    bvh_ray_node(sc, q, nd, true, minT * dn, st, [&](unsigned i) {
+    const int nx = bvh_ray_node(sc, q, nd, true, minT * dn, st, [&](unsigned i, V3 ce, float r2) {
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
-      float r2;
-      const V3 ce = sc.sphere(i, r2);
       bool res;
       const float t = ray_sphere(q, ce, r2, res);
       if (res && (t < minT || (t == minT && (int)i < best))) {
@@ -1273,6 +1303,12 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
         best = (int)i;
       }
     });
+    if (nx > 0) {
+      nd = (unsigned)nx;
+    } else {
+      if (st.empty()) break;
+      nd = (unsigned)st.pop();
+    }
   }
   tOut = minT;
   return best;
@@ -1284,16 +1320,12 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   const float reach = norm_up(gap);
   sc.count(kCntBvhShadowQ, 1);
   BvhStack st(sc.bvh_stack());
-  st.push(0);
-  while (!st.empty()) {  // wave-uniform
-    if (sc.all(blk)) break;
-    const unsigned nd = (unsigned)st.pop();
+  unsigned nd = 0;  // the root
+  for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
-    bvh_ray_node(sc, q, nd, !blk, reach, st, [&](unsigned i) {
+    const int nx = bvh_ray_node(sc, q, nd, !blk, reach, st, [&](unsigned, V3 ce, float r2) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
-      float r2;
-      const V3 ce = sc.sphere(i, r2);
       bool res;
       const float t = ray_sphere(q, ce, r2, res);
       if (res && t < 1000.f) {
@@ -1301,6 +1333,13 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
         if (vdot(dist, dist) < gap) blk = true;
       }
     }, true);
+    if (sc.all(blk)) break;
+    if (nx > 0) {
+      nd = (unsigned)nx;
+    } else {
+      if (st.empty()) break;
+      nd = (unsigned)st.pop();
+    }
   }
   return blk;
 }
@@ -1312,26 +1351,32 @@ template <class Scene>
 RTG_HD int container_bvh(const Scene& sc, V3 pt) {
   int found = 0x7FFFFFFF;
   BvhStack st(sc.bvh_stack());
-  st.push(0);
-  while (!st.empty()) {  // wave-uniform
-    const int nd = st.pop();
+  unsigned nd = 0;  // the root
+  for (;;) {        // wave-uniform
     sc.count(kUContBvhNode, 1);
-    V3 c[4];
-    float w[4], rp[4], cr[4];
-    int ch[4];
-    sc.bvh_node((unsigned)nd, c, w, ch);
-    sc.bvh_aux((unsigned)nd, rp, cr);
+    BvhRec r;
+    sc.bvh_rec(nd, r);
+    int nxt = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int x = ch[k];
+      const int x = r.ch[k];
       if (x == 0) continue;
-      const V3 dist = vsub(pt, c[k]);
-      const bool in = vdot(dist, dist) <= cr[k];
+      const V3 dist = vsub(pt, v3(r.g[4 * k], r.g[4 * k + 1], r.g[4 * k + 2]));
+      const bool in = vdot(dist, dist) <= r.aux[2 * k + 1];
       if (x > 0) {
-        if (sc.any(in)) st.push(x);
+        if (sc.any(in)) {  // the last such child is the next node, no stack round trip
+          if (nxt > 0) st.push(nxt);
+          nxt = x;
+        }
       } else if (in && (int)~x < found) {
         found = (int)~x;
       }
+    }
+    if (nxt > 0) {
+      nd = (unsigned)nxt;
+    } else {
+      if (st.empty()) break;
+      nd = (unsigned)st.pop();
     }
   }
   return found == 0x7FFFFFFF ? -1 : found;

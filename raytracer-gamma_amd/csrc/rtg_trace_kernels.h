@@ -159,8 +159,6 @@ struct DevScene {
   cfloat_p prim;  // n x {1/|c|, sin a, cos a, 0}: primary-cull sphere constants
   cfloat_p bvhNodes;  // BVH (build_bvh, rtg_scene_pack.h) or null
   int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
-  cfloat_p bvhAux;
-  const RTG_CONST int* bvhChild;
   unsigned n, m;
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
@@ -212,22 +210,19 @@ struct DevScene {
     else return false;
   }
   __device__ __forceinline__ int* bvh_stack() const { return bvhStk; }
-  __device__ __forceinline__ void bvh_node(unsigned nd, V3* c, float* w, int* ch) const {
-    cfloat_p g = bvhNodes + 16 * nd;
-    const RTG_CONST int* h = bvhChild + 4 * nd;
+  // Node nd's record (BvhRec, rtg_trace.h): two 64-byte scalar loads.
+  __device__ __forceinline__ void bvh_rec(unsigned nd, BvhRec& r) const {
+    typedef float f16 __attribute__((ext_vector_type(16)));
+    const RTG_CONST f16* p = (const RTG_CONST f16*)fidx(bvhNodes, kBvhWords * nd);
+    const f16 a = p[0], b = p[1];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r.g[k] = a[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.aux[k] = b[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      c[k] = v3(g[4 * k + 0], g[4 * k + 1], g[4 * k + 2]);
-      w[k] = g[4 * k + 3];
-      ch[k] = h[k];
-    }
-  }
-  __device__ __forceinline__ void bvh_aux(unsigned nd, float* rp, float* cr) const {
-    cfloat_p g = bvhAux + 8 * nd;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      rp[k] = g[2 * k];
-      cr[k] = g[2 * k + 1];
+      r.ch[k] = __float_as_int(b[8 + k]);
+      r.r2[k] = b[12 + k];
     }
   }
   // One lane's value for wave-uniform decisions (traversal order, cone cull).
@@ -407,9 +402,7 @@ struct KernelArgs {
   const unsigned* smask;  // shadow masks (PackedScene::smask) or null
   const unsigned* cone;   // cone masks (PackedScene::cone) or null
   const float* prim;      // primary-cull sphere constants (PackedScene::prim)
-  const float* bvhNodes;  // BVH (PackedScene::bvh*) or null
-  const float* bvhAux;
-  const int* bvhChild;
+  const float* bvhNodes;  // BVH node records (PackedScene::bvhNodes) or null
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
@@ -510,8 +503,6 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   // (the launcher adds them to the LDS size).
   sc.bvhStk = reinterpret_cast<int*>(sceneLds + (kLds ? (a.n + 1) * 2 + a.n4 : 0)) +
               (threadIdx.x >> 6) * 64;
-  sc.bvhAux = (cfloat_p)a.bvhAux;
-  sc.bvhChild = (const RTG_CONST int*)a.bvhChild;
   sc.n = a.n;
   sc.m = a.m;
   sc.n4 = a.n4;

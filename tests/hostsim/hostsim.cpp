@@ -31,8 +31,6 @@ struct HostScene {
   bool any(bool b) const { return b; }
   int fuse = 0;  // fused query forms (rtg_trace.h kFuse*), set per variant
   const float* bvhNodes = nullptr;
-  const float* bvhAux = nullptr;
-  const int* bvhChild = nullptr;
   bool has_bvh() const { return bvhNodes != nullptr; }
   const float* prim = nullptr;
   const unsigned* cone = nullptr;
@@ -44,19 +42,12 @@ struct HostScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   int* bvh_stack() const { return nullptr; }
-  void bvh_node(unsigned nd, rtg::V3* c, float* w, int* ch) const {
-    for (int k = 0; k < 4; ++k) {
-      const float* g = bvhNodes + 16 * nd + 4 * k;
-      c[k] = rtg::v3(g[0], g[1], g[2]);
-      w[k] = g[3];
-      ch[k] = bvhChild[4 * nd + k];
-    }
-  }
-  void bvh_aux(unsigned nd, float* rp, float* cr) const {
-    for (int k = 0; k < 4; ++k) {
-      rp[k] = bvhAux[8 * nd + 2 * k];
-      cr[k] = bvhAux[8 * nd + 2 * k + 1];
-    }
+  void bvh_rec(unsigned nd, rtg::BvhRec& r) const {
+    const float* g = bvhNodes + (size_t)rtg::kBvhWords * nd;
+    memcpy(r.g, g, 16 * 4);
+    memcpy(r.aux, g + 16, 8 * 4);
+    memcpy(r.ch, g + 24, 4 * 4);
+    memcpy(r.r2, g + 28, 4 * 4);
   }
   float first_lane(float v) const { return v; }
   rtg::V3 sphere(unsigned i, float& r2) const {
@@ -245,10 +236,8 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
   sc.fuse = (g_variant == 0 || g_variant == 15 || g_variant == 50)
                 ? (rtg::kFusePrim | rtg::kFuseCone | rtg::kFuseShadow | rtg::kFuseEnter)
                 : 0;
-  if (!ps.bvhChild.empty() && g_useBvh) {
+  if (!ps.bvhNodes.empty() && g_useBvh) {
     sc.bvhNodes = ps.bvhNodes.data();
-    sc.bvhAux = ps.bvhAux.data();
-    sc.bvhChild = ps.bvhChild.data();
   }
   for (unsigned k = 0; k < nrows; ++k) {
     float* o = out + (size_t)k * W * 3;
