@@ -207,6 +207,9 @@ def main():
     sptr = stream.cuda_stream
     ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for _ in range(args.steps)]
+    # N > 1, rank 0: gather complete (after the waits) and assemble done
+    ev_g = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     # N > 1: chunks of the padded shard (same row ranges on every rank); the
     # global rows of this rank's real rows, for rtg_render_rows_device.
     K = max(1, min(args.gather_chunks, Rmax)) if world > 1 else 1
@@ -252,6 +255,8 @@ def main():
             ev_k[i][1].record(stream)
         for w in works:
             w.wait()
+        if i is not None:
+            ev_g[i].record(stream)
         if rank == 0:
             if args.dist_backend == "nccl":  # native permute kernel on the device
                 ctx.assemble_shards_device(gathered.data_ptr(), world, Rmax, W, H, B,
@@ -259,6 +264,8 @@ def main():
                 frame = frame_buf
             else:
                 frame = rdist.assemble(gathered, H, B).contiguous()
+        if i is not None:
+            ev_a[i].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -280,11 +287,28 @@ def main():
         kern_ms = ev_region[0].elapsed_time(ev_region[1]) / args.steps
     else:
         kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_k]))
+    multi = None
     if world > 1:
         dev = "cuda" if args.dist_backend == "nccl" else "cpu"
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_max_ms = float(t[0]), float(t[1])
+        # every rank's render time (its shard's chunks, HIP events), on rank 0
+        mine = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [round(float(x[0]), 4) for x in allr]
+        gather_tail = float(np.mean([ev_k[i][1].elapsed_time(ev_g[i]) for i in range(args.steps)]))
+        assemble = float(np.mean([ev_g[i].elapsed_time(ev_a[i]) for i in range(args.steps)]))
+        multi = {"render_ms_per_rank": per_rank,
+                 "render_imbalance": round(max(per_rank) / (sum(per_rank) / world), 4),
+                 "gather_tail_ms_rank0": round(gather_tail, 4),
+                 "assemble_ms_rank0": round(assemble, 4),
+                 "step_ms": round(elapsed / args.steps * 1e3, 4),
+                 "note": "render = this rank's shard chunks (HIP events); gather tail = end of "
+                         "rank 0's render to the last gathered chunk on its stream (the gathers "
+                         "of earlier chunks overlap rendering); assemble = row-order restore "
+                         "on rank 0; step = wall time per frame, max over ranks"}
     else:
         kern_max_ms = kern_ms
 
@@ -512,7 +536,7 @@ def main():
                         else " + gloo gather") if world > 1 else "")},
         "mrays_per_s": round(mpx * 9, 1),
         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
-        "roofline": roof, "cpu_baseline": cpu, "e2e": e2e,
+        "roofline": roof, "cpu_baseline": cpu, "e2e": e2e, "multi_gpu": multi,
         "gpu_vs_cpu": round(mpx / cpu["value"], 1) if cpu else None,
         "parity": parity,
         "ab": ab,

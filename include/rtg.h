@@ -117,6 +117,15 @@ int rtg_multi_render(rtg_multi* mg, unsigned width, unsigned height, float zoom,
                      float aliasFactor, int stackSize, unsigned rowBlock, rtg_vec* dstHost,
                      float* timingsMs);
 int rtg_multi_destroy(rtg_multi* mg);
+/* How rtg_multi_render brings the shards to the root:
+ * RTG_GATHER_RCCL (default): one grouped ncclGather of the padded shards, then
+ * the assemble kernel; RTG_GATHER_PEER_COPY (ablation): no collective, no
+ * assemble — every device writes its shard's row blocks straight into the
+ * root's frame with one strided peer copy (rtg_place_shard_device); needs
+ * peer access to the root (enabled here, or RTG_ERR_HIP). */
+#define RTG_GATHER_RCCL 0
+#define RTG_GATHER_PEER_COPY 1
+int rtg_multi_set_gather(rtg_multi* mg, int mode);
 
 /* ---- persistent context: scene resident in HBM, caller-owned streams ---- */
 typedef struct rtg_context rtg_context;
@@ -158,6 +167,15 @@ int rtg_render_device(rtg_context* ctx, unsigned width, unsigned height, float z
 int rtg_assemble_shards_device(rtg_context* ctx, const rtg_vec* gathered, unsigned nShards,
                                unsigned paddedRows, unsigned width, unsigned height,
                                unsigned rowBlock, rtg_vec* frame, void* stream);
+
+/* The inverse placement without a gather buffer: copy shard `shardIdx`'s
+ * packed rows (as rtg_render_device packs them) into their rows of the
+ * height x width `frame` with one strided copy (hipMemcpy2DAsync; `frame` may
+ * be another device's memory with peer access) plus one copy for a ragged
+ * last block, on `stream`. */
+int rtg_place_shard_device(rtg_context* ctx, const rtg_vec* shard, unsigned shardIdx,
+                           unsigned nShards, unsigned width, unsigned height, unsigned rowBlock,
+                           rtg_vec* frame, void* stream);
 
 /* Render an explicit list of global rows (each < height) into dstDevice
  * (nRows * width rtg_vec, in list order); rowsDevice is device memory. */

@@ -718,7 +718,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
                   RTG_MAX_STACK, variant);
     return RTG_ERR_INVALID;
   }
-  const size_t frameLds = (size_t)(stackSize > 1 ? stackSize - 1 : 1) * threads * 16;
+  const size_t frameLds =
+      (size_t)frame_lds_levels(stackSize, ctx->bvhNodes != nullptr) * threads * 16;
   const size_t lds = frameLds +
                      (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) + (size_t)ctx->n4 * 16)
                               : 0) +
@@ -894,6 +895,38 @@ int rtg_assemble_shards_device(rtg_context* ctx, const rtg_vec* gathered, unsign
                        (const unsigned*)gathered, (unsigned*)frame, nShards, paddedRows, height,
                        rowBlock, rowBytes / 4);
   HIP_TRY(hipGetLastError());
+  return RTG_OK;
+}
+
+int rtg_place_shard_device(rtg_context* ctx, const rtg_vec* shard, unsigned shardIdx,
+                           unsigned nShards, unsigned width, unsigned height, unsigned rowBlock,
+                           rtg_vec* frame, void* stream) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
+  rtg_clear_error();
+  if (!ctx || !shard || !frame || nShards == 0 || shardIdx >= nShards || rowBlock == 0 ||
+      width == 0 || height == 0) {
+    rtg_set_error("rtg_place_shard_device: invalid arguments");
+    return RTG_ERR_INVALID;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  // shard block j holds global row block j G + g (rtg_shard_rows packing)
+  const size_t nb = (height + rowBlock - 1) / rowBlock;
+  const size_t rowBytes = (size_t)width * sizeof(rtg_vec);
+  const size_t blockBytes = rowBytes * rowBlock;
+  const size_t fullBlocks = height / rowBlock;  // global blocks of rowBlock rows
+  size_t nFull = 0;                             // this shard's full blocks
+  if (fullBlocks > shardIdx) nFull = (fullBlocks - shardIdx + nShards - 1) / nShards;
+  hipStream_t st = (hipStream_t)stream;
+  if (nFull > 0)
+    HIP_TRY(hipMemcpy2DAsync((char*)frame + (size_t)shardIdx * blockBytes,
+                             blockBytes * nShards, shard, blockBytes, blockBytes, nFull,
+                             hipMemcpyDeviceToDevice, st));
+  const size_t gb = nFull * nShards + shardIdx;  // a ragged last block of this shard
+  if (gb < nb) {
+    const size_t rows = height - gb * rowBlock;
+    HIP_TRY(hipMemcpyAsync((char*)frame + gb * blockBytes, (const char*)shard + nFull * blockBytes,
+                           rows * rowBytes, hipMemcpyDeviceToDevice, st));
+  }
   return RTG_OK;
 }
 

@@ -13,6 +13,12 @@
 // rtg_multi_* keep the communicator, the per-device contexts, streams and
 // buffers across frames (ncclCommInitAll costs ~0.5 s); rtg_render_multi is
 // the one-shot form.
+//
+// Ablation (rtg_multi_set_gather(RTG_GATHER_PEER_COPY)): no
+// collective and no assemble pass; each device places its shard's row blocks
+// straight into the root's frame with ONE strided peer copy
+// (rtg_place_shard_device, hipMemcpy2DAsync over xGMI), and the root waits for
+// every device's copy before the read-back.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -33,12 +39,14 @@ struct Dev {
   rtg_vec* shard = nullptr;
   size_t shardCap = 0;  // rtg_vec
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEvent_t ec = nullptr;  // peer-copy mode: this device's copy into the root's frame is done
 };
 
 }  // namespace
 
 struct rtg_multi {
   std::vector<Dev> d;
+  int gather = RTG_GATHER_RCCL;  // RTG_GATHER_* (rtg_multi_set_gather)
   rtg_vec* gathered = nullptr;  // on devices[0]
   rtg_vec* frame = nullptr;
   size_t gatheredCap = 0, frameCap = 0;
@@ -66,6 +74,7 @@ int rtg_multi_destroy(rtg_multi* mg) {
     (void)hipFree(v.shard);
     if (v.e0) (void)hipEventDestroy(v.e0);
     if (v.e1) (void)hipEventDestroy(v.e1);
+    if (v.ec) (void)hipEventDestroy(v.ec);
     if (v.stream) (void)hipStreamDestroy(v.stream);
     rtg_context_destroy(v.ctx);
   }
@@ -109,7 +118,8 @@ int rtg_multi_create(const int* devices, int nDevices, rtg_multi** out) {
     }
     if (hipSetDevice(v.id) != hipSuccess ||
         hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&v.e0) != hipSuccess || hipEventCreate(&v.e1) != hipSuccess) {
+        hipEventCreate(&v.e0) != hipSuccess || hipEventCreate(&v.e1) != hipSuccess ||
+        hipEventCreateWithFlags(&v.ec, hipEventDisableTiming) != hipSuccess) {
       rtg_multi_destroy(mg);
       rtg_set_error("rtg_multi_create: stream/event creation failed");
       return RTG_ERR_HIP;
@@ -129,6 +139,36 @@ int rtg_multi_create(const int* devices, int nDevices, rtg_multi** out) {
   }
   for (int g = 0; g < nDevices; ++g) mg->d[(size_t)g].comm = comms[(size_t)g];
   *out = mg;
+  return RTG_OK;
+}
+
+int rtg_multi_set_gather(rtg_multi* mg, int mode) {
+  rtg::DeviceGuard deviceGuard;  // the caller's current device is restored on return
+  rtg_clear_error();
+  if (!mg || (mode != RTG_GATHER_RCCL && mode != RTG_GATHER_PEER_COPY)) {
+    rtg_set_error("rtg_multi_set_gather: invalid arguments");
+    return RTG_ERR_INVALID;
+  }
+  if (mode == RTG_GATHER_PEER_COPY) {  // the root's frame must be writable by every device
+    const int root = mg->d[0].id;
+    for (size_t g = 1; g < mg->d.size(); ++g) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, mg->d[g].id, root) != hipSuccess || !can) {
+        rtg_set_error("rtg_multi_set_gather: device %d cannot access device %d", mg->d[g].id,
+                      root);
+        return RTG_ERR_HIP;
+      }
+      (void)hipSetDevice(mg->d[g].id);
+      const hipError_t e = hipDeviceEnablePeerAccess(root, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        rtg_set_error("rtg_multi_set_gather: peer access %d -> %d: %s", mg->d[g].id, root,
+                      hipGetErrorString(e));
+        return RTG_ERR_HIP;
+      }
+      (void)hipGetLastError();  // clear an "already enabled" status
+    }
+  }
+  mg->gather = mode;
   return RTG_OK;
 }
 
@@ -183,7 +223,8 @@ int rtg_multi_render(rtg_multi* mg, unsigned width, unsigned height, float zoom,
   }
   Dev& root = mg->d[0];
   (void)hipSetDevice(root.id);
-  if (mg->gatheredCap < shardElems * G) {
+  const bool peer = mg->gather == RTG_GATHER_PEER_COPY;
+  if (!peer && mg->gatheredCap < shardElems * G) {
     (void)hipFree(mg->gathered);
     mg->gathered = nullptr;
     mg->gatheredCap = 0;
@@ -212,8 +253,28 @@ int rtg_multi_render(rtg_multi* mg, unsigned width, unsigned height, float zoom,
     rc = rtg_render_device(v.ctx, width, height, zoom, aliasFactor, stackSize, rowBlock, g, G,
                            v.shard, v.stream);
     (void)hipEventRecord(v.e1, v.stream);
+    if (rc == RTG_OK && peer) {  // the shard's blocks straight into the root's frame
+      rc = rtg_place_shard_device(v.ctx, v.shard, g, G, width, height, rowBlock, mg->frame,
+                                  v.stream);
+      if (rc == RTG_OK && g > 0 && hipEventRecord(v.ec, v.stream) == hipSuccess) {
+        (void)hipSetDevice(root.id);  // the root's stream waits for this copy
+        if (hipStreamWaitEvent(root.stream, v.ec, 0) != hipSuccess) {
+          rtg_set_error("rtg_multi_render: stream wait failed");
+          rc = RTG_ERR_HIP;
+        }
+      }
+    }
   }
-  if (rc == RTG_OK) {  // ONE grouped gather of the padded shards to the root
+  if (rc == RTG_OK && peer) {
+    (void)hipSetDevice(root.id);
+    if (hipEventRecord(mg->g1, root.stream) != hipSuccess ||
+        hipMemcpyAsync(dstHost, mg->frame, frameElems * sizeof(rtg_vec), hipMemcpyDeviceToHost,
+                       root.stream) != hipSuccess) {
+      rtg_set_error("rtg_multi_render: frame readback failed");
+      rc = RTG_ERR_HIP;
+    }
+  }
+  if (rc == RTG_OK && !peer) {  // ONE grouped gather of the padded shards to the root
     ncclResult_t nr = ncclGroupStart();
     for (unsigned g = 0; g < G && nr == ncclSuccess; ++g)
       nr = ncclGather(mg->d[g].shard, g == 0 ? (void*)mg->gathered : nullptr, shardElems * 3,
@@ -225,7 +286,7 @@ int rtg_multi_render(rtg_multi* mg, unsigned width, unsigned height, float zoom,
       rc = RTG_ERR_HIP;
     }
   }
-  if (rc == RTG_OK) {
+  if (rc == RTG_OK && !peer) {
     (void)hipSetDevice(root.id);
     rc = rtg_assemble_shards_device(root.ctx, mg->gathered, G, Rmax, width, height, rowBlock,
                                     mg->frame, root.stream);

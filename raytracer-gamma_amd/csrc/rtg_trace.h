@@ -250,10 +250,12 @@ struct FrameR { V3 ro, rd, rI; };
 
 // Local (private-memory) storage of the colour part, used when the scene does
 // not provide per-lane LDS frames.
+// Frame stores provide get(lv) / set(lv, frame) (trace_sample).
 template <int NF>
 struct LocalFrames {
   FrameC f[NF];
-  RTG_HD FrameC& operator()(int lv) { return f[lv]; }
+  RTG_HD FrameC get(int lv) const { return f[lv]; }
+  RTG_HD void set(int lv, const FrameC& v) { f[lv] = v; }
 };
 
 // One ancestor frame.
@@ -874,12 +876,13 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         if (!leaf) {
           sc.probe_begin(kProbePush);
           const int lv = sp < NF ? sp : NF - 1;
-          FrameC& f = fc(lv);
+          FrameC f;
           f.cx = colour.x; f.cy = colour.y; f.cz = colour.z;
           // bits 2..8: 1 + the sphere whose origin ball holds the
           // reflection ray's origin P + 0.01 rd (cone cull, n <= 64), or 0
           f.meta = ((unsigned)rm << 9) |
                    ((unsigned)(sc.has_cone() && guardOK ? hit + 1 : 0) << 2) | (sigR ? 2u : 0u);
+          fc.set(lv, f);
           if (sigR) {
             sc.count(kCntReflPush, 1);
             sc.count(kUPush, 1);
@@ -921,12 +924,13 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     while (sp > 0) {
       sc.count(kUUnwind, 1);
       const int lv = sp - 1 < NF ? sp - 1 : NF - 1;
-      FrameC& f = fc(lv);
+      FrameC f = fc.get(lv);
       const V3 fcol = vadd(ret, v3(f.cx, f.cy, f.cz));        // :553 / :622
       ret = fcol;                                             // :617 / :626
       if ((f.meta & 3u) == 2u) {                              // stage 1, reflection
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
+        fc.set(lv, f);
         o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 9);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845

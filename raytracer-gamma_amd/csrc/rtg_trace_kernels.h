@@ -57,7 +57,27 @@ __device__ __forceinline__ const float* fidx(const float* p, unsigned i) { retur
 template <int kThreads>
 struct LdsFrames {
   FrameC* base;  // already offset by threadIdx.x
-  __device__ __forceinline__ FrameC& operator()(int lv) const { return base[lv * kThreads]; }
+  __device__ __forceinline__ FrameC get(int lv) const { return base[lv * kThreads]; }
+  __device__ __forceinline__ void set(int lv, const FrameC& v) const { base[lv * kThreads] = v; }
+};
+// The same with the deepest level `top` in four VGPRs instead of LDS (BVH
+// kernels, stack capacity >= 3): one KiB less LDS per wave, which is what
+// limits their occupancy (7 frame levels + the traversal stack at S = 8: 5
+// waves per SIMD; 6 with this).  Level `top` holds a frame only while a node
+// of depth S - 1 (a leaf) is being shaded below it.
+template <int kThreads>
+struct LdsFramesTop {
+  FrameC* base;  // already offset by threadIdx.x; levels 0 .. top-1
+  int top;
+  mutable FrameC reg;
+  __device__ __forceinline__ FrameC get(int lv) const {
+    const FrameC l = base[(lv < top ? lv : top - 1) * kThreads];
+    return lv < top ? l : reg;
+  }
+  __device__ __forceinline__ void set(int lv, const FrameC& v) const {
+    if (lv < top) base[lv * kThreads] = v;
+    else reg = v;
+  }
 };
 
 // kBvh: the kernel instantiation for BVH scenes (n > 64); without it the BVH
@@ -75,11 +95,16 @@ template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = f
           int kFuse = 0, bool kMasks = false, bool kCount = false>
 struct DevScene {
   static constexpr int fuse = kFuse;
+  static constexpr bool kIsBvh = kBvh;
   FrameC* lfr;
   __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
   __device__ __forceinline__ bool any(bool b) const { return __ballot(b) != 0ull; }
-  __device__ __forceinline__ LdsFrames<kThreads> frames() const {
-    return LdsFrames<kThreads>{lfr};
+  // frame levels 0 .. nfl-1 in LDS (nfl = frame_lds_levels); BVH kernels keep
+  // the deepest of NF levels in VGPRs (LdsFramesTop)
+  int nfl;
+  __device__ __forceinline__ auto frames() const {
+    if constexpr (kBvh) return LdsFramesTop<kThreads>{lfr, nfl, FrameC{}};
+    else return LdsFrames<kThreads>{lfr};
   }
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
@@ -471,13 +496,22 @@ struct MinWaves {
       : ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
 };
 
+// Frame levels in LDS per lane: S - 1 ancestors (at least 1: the pixel sum
+// parks samples in level 0), one fewer for BVH kernels from S = 3 on
+// (LdsFramesTop keeps the deepest in VGPRs).  launch_trace sizes the LDS with
+// the same rule.
+constexpr int frame_lds_levels(int S, bool bvh) {
+  return (S > 1 ? S - 1 : 1) - ((bvh && S >= 3) ? 1 : 0);
+}
+
 // Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
 template <int S, bool kLds, int kThreads, class Sc>
 __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   extern __shared__ float4 lds4[];
-  constexpr int NF = (S > 1) ? (S - 1) : 1;
+  constexpr int NFL = frame_lds_levels(S, Sc::kIsBvh);
   sc.lfr = reinterpret_cast<FrameC*>(lds4) + threadIdx.x;
-  float4* sceneLds = lds4 + NF * kThreads;
+  sc.nfl = NFL;
+  float4* sceneLds = lds4 + NFL * kThreads;
   if constexpr (kLds) {
     float* lmats = reinterpret_cast<float*>(sceneLds);
     const unsigned nm = (a.n + 1) * 8;

@@ -60,6 +60,7 @@ EXPORTED = [
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate", "rtg_assemble_shards_device",
     "rtg_render_multi", "rtg_scene_load", "rtg_scene_save", "rtg_context_set_semantics",
     "rtg_multi_create", "rtg_multi_set_scene", "rtg_multi_render", "rtg_multi_destroy",
+    "rtg_multi_set_gather", "rtg_place_shard_device",
 ]
 
 
@@ -125,6 +126,8 @@ def lib() -> ctypes.CDLL:
         L.rtg_multi_set_scene.argtypes = [vp, vp, u, vp, u]
         L.rtg_multi_render.argtypes = [vp, u, u, f, f, i, u, vp, vp]
         L.rtg_multi_destroy.argtypes = [vp]
+        L.rtg_multi_set_gather.argtypes = [vp, i]
+        L.rtg_place_shard_device.argtypes = [vp, vp, u, u, u, u, u, vp, vp]
         pu = ctypes.POINTER(u)
         L.rtg_scene_load.argtypes = [ctypes.c_char_p, vp, u, pu, vp, u, pu]
         L.rtg_scene_save.argtypes = [ctypes.c_char_p, vp, u, vp, u]
@@ -290,6 +293,12 @@ class MultiContext:
         _check(lib().rtg_multi_set_scene(self._h, _ptr(self._sph), len(self._sph),
                                          _ptr(self._lgt), len(self._lgt)), "rtg_multi_set_scene")
 
+    GATHER_RCCL, GATHER_PEER_COPY = 0, 1  # RTG_GATHER_*
+
+    def set_gather(self, mode: int):
+        """RCCL gather + assemble (default) or the peer-copy ablation."""
+        _check(lib().rtg_multi_set_gather(self._h, int(mode)), "rtg_multi_set_gather")
+
     def render(self, width, height, zoom=-4.0, alias_factor=3.0, stack_size=6, row_block=16):
         out = np.empty((height, width, 3), np.float32)
         tm = np.zeros(3, np.float32)
@@ -432,6 +441,14 @@ class Context:
                                                 ctypes.c_void_p(frame_ptr),
                                                 ctypes.c_void_p(stream) if stream else None),
                "rtg_assemble_shards_device")
+
+    def place_shard_device(self, shard_ptr: int, shard: int, n_shards: int, width: int,
+                           height: int, row_block: int, frame_ptr: int, stream: int = 0):
+        """Copy one shard's packed rows into their rows of a frame (rtg_place_shard_device)."""
+        _check(lib().rtg_place_shard_device(self._h, ctypes.c_void_p(shard_ptr), shard, n_shards,
+                                            width, height, row_block, ctypes.c_void_p(frame_ptr),
+                                            ctypes.c_void_p(stream) if stream else None),
+               "rtg_place_shard_device")
 
     def ppm_bytes_device(self, src_ptr: int, n_pixels: int, max_ptr: int, dst_ptr: int,
                          stream: int = 0):

@@ -67,7 +67,8 @@ struct HostScene {
   void probe_begin(int) const {}
   struct Frames {
     rtg::FrameC* f;
-    rtg::FrameC& operator()(int lv) const { return f[lv]; }
+    rtg::FrameC get(int lv) const { return f[lv]; }
+    void set(int lv, const rtg::FrameC& v) const { f[lv] = v; }
   };
   mutable rtg::FrameC fr[16];
   Frames frames() const { return Frames{fr}; }

@@ -200,6 +200,13 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
         ctx.assemble_shards_device(buf.data_ptr(), G, Rmax, W, H, B, frame.data_ptr(), stream)
         torch.cuda.synchronize()
         assert canon_md5(frame.cpu().numpy()) == c["fb_md5"], G
+        # the peer-copy ablation's placement (rtg_place_shard_device): every
+        # shard straight into its rows of the frame, no gather buffer
+        frame.fill_(7.0)
+        for g in range(G):
+            ctx.place_shard_device(buf[g].data_ptr(), g, G, W, H, B, frame.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert canon_md5(frame.cpu().numpy()) == c["fb_md5"], ("place", G)
     # odd widths take the 4-byte copy path; 16-byte path for W % 4 == 0
     for (W2, H2, G, B2) in [(37, 29, 3, 4), (64, 33, 5, 8), (1, 7, 2, 1)]:
         Rmax = dist.padded_rows(H2, B2, G)
@@ -209,6 +216,11 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
         torch.cuda.synchronize()
         want = dist.assemble(buf.cpu().numpy(), H2, B2)
         assert np.array_equal(frame.cpu().numpy(), want), (W2, H2, G, B2)
+        frame.fill_(-1.0)
+        for g in range(G):
+            ctx.place_shard_device(buf[g].data_ptr(), g, G, W2, H2, B2, frame.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy(), want), ("place", W2, H2, G, B2)
     ctx.close()
 
 
@@ -407,6 +419,16 @@ def _render_multi_checks(R, golden, devs):
         assert canon_md5(fb) == c["fb_md5"]
     small, _ = mc.render(40, 30, stack_size=c["stack_size"])
     assert bits_equal(small, R.render(sph, lg, 40, 30, stack_size=c["stack_size"]))
+    # the peer-copy ablation (no collective, no assemble pass)
+    mc.set_gather(mc.GATHER_PEER_COPY)
+    for B in (16, 8, 7):
+        fb, tm = mc.render(c["W"], c["H"], stack_size=c["stack_size"], row_block=B)
+        assert canon_md5(fb) == c["fb_md5"], ("peer", devs, B)
+    mc.set_gather(mc.GATHER_RCCL)
+    fb, _ = mc.render(c["W"], c["H"], stack_size=c["stack_size"])
+    assert canon_md5(fb) == c["fb_md5"]
+    with pytest.raises(R.RtgError):
+        mc.set_gather(5)
     mc.close()
     with pytest.raises(R.RtgError):
         R.render_multi(sph, lg, 8, 8, devices=[0, 0])
