@@ -224,6 +224,10 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kUUnwind,      // one unwind step (stage 1/2 colour sums)
              kUSample,      // one primary sample: ray set-up, cull hand-over, pixel sum
              kUBvhPass,     // (diagnostic) a BVH child-node screen passes for the lane
+             kUDiagShdSame,   // (diagnostic) shadow query, every lane on one hit sphere
+             kUDiagEnterAll,  // (diagnostic) closest query, every lane's ray entered a sphere
+             kUDiagEnterSame, // (diagnostic) ... the same sphere
+             kUDiagContSame,  // (diagnostic) refraction target query, one hit sphere
              kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
@@ -573,6 +577,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
           sc.count(kCntShadowSel, __builtin_popcountll(su));
           blk = blocked_sel(sc, P, dir, gap, su);
         } else {
+          if (sc.has_bvh() && sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagShdSame, 1);
           blk = query_blocked<2>(sc, P, dir, gap);
         }
       } else {
@@ -700,6 +705,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
     tgt = primary_container_sel(sc, testPt, cu, nTgt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
   } else {
+    if (sc.has_bvh() && sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagContSame, 1);
     sc.count(kCntContainFull, 1);
     tgt = primary_container(sc, testPt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
@@ -820,6 +826,10 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         hit = query_closest<2>(sc, o, d, t);
       }
     } else {
+      if (sc.has_bvh() && sc.all(enterH >= 0)) {
+        sc.count(kUDiagEnterAll, 1);
+        if (sc.all(sc.first_lane_i(enterH) == enterH)) sc.count(kUDiagEnterSame, 1);
+      }
       sc.count(kCntFullQ, 1);
       hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
     }

@@ -254,6 +254,9 @@ struct DevScene {
   __device__ __forceinline__ float first_lane(float v) const {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
   }
+  __device__ __forceinline__ int first_lane_i(int v) const {
+    return __builtin_amdgcn_readfirstlane(v);
+  }
   __device__ __forceinline__ V3 first_lane(V3 v) const {
     return v3(first_lane(v.x), first_lane(v.y), first_lane(v.z));
   }

@@ -76,6 +76,7 @@ UNIT_NAMES = [
     "U.bvhNode", "U.bvhSlot", "U.bvhExact", "U.contIter", "U.cont4", "U.contBvhNode", "U.cone",
     "U.maskIter", "U.node", "U.shade", "U.light", "U.shadow", "U.lit", "U.refr", "U.refrLeaf",
     "U.push", "U.descend", "U.unwind", "U.sample", "U.bvhPass",
+    "D.shdSame", "D.enterAll", "D.enterSame", "D.contSame",
 ]
 
 
@@ -112,8 +113,17 @@ def lib() -> ctypes.CDLL:
         L.rtg_context_set_semantics.argtypes = [vp, i]
         L.rtg_diag_read.argtypes = [vp, vp, i]
         L.rtg_diag_timeline.argtypes = [vp, vp, sz, vp]
-        L.rtg_diag_counts.argtypes = [vp, vp, i, i]
-        L.rtg_context_scene_stats.argtypes = [vp, vp]
+        # round-3 entry points; an RTG_LIB build from before them (same-box A/B
+        # of older kernels, tools/ab_bench.sh) loads without them
+        for name, at in (("rtg_diag_counts", [vp, vp, i, i]),
+                         ("rtg_context_scene_stats", [vp, vp]),
+                         ("rtg_multi_set_gather", [vp, i]),
+                         ("rtg_place_shard_device", [vp, vp, u, u, u, u, u, vp, vp])):
+            try:
+                getattr(L, name).argtypes = at
+            except AttributeError:
+                if not os.environ.get("RTG_LIB"):
+                    raise
         L.rtg_max_colour.argtypes = [vp, sz]
         L.rtg_max_colour.restype = f
         L.rtg_max_colour_device.argtypes = [vp, vp, sz, vp, vp]
@@ -126,8 +136,7 @@ def lib() -> ctypes.CDLL:
         L.rtg_multi_set_scene.argtypes = [vp, vp, u, vp, u]
         L.rtg_multi_render.argtypes = [vp, u, u, f, f, i, u, vp, vp]
         L.rtg_multi_destroy.argtypes = [vp]
-        L.rtg_multi_set_gather.argtypes = [vp, i]
-        L.rtg_place_shard_device.argtypes = [vp, vp, u, u, u, u, u, vp, vp]
+
         pu = ctypes.POINTER(u)
         L.rtg_scene_load.argtypes = [ctypes.c_char_p, vp, u, pu, vp, u, pu]
         L.rtg_scene_save.argtypes = [ctypes.c_char_p, vp, u, vp, u]
@@ -362,6 +371,8 @@ class Context:
 
     def scene_stats(self):
         """{prep_ms, upload_ms, device_bytes, bvh_nodes} of the last set_scene."""
+        if not hasattr(lib(), "rtg_context_scene_stats"):  # an older RTG_LIB build
+            return {"prep_ms": 0.0, "upload_ms": 0.0, "device_bytes": 0, "bvh_nodes": 0}
         out = (ctypes.c_double * 4)()
         _check(lib().rtg_context_scene_stats(self._h, ctypes.cast(out, ctypes.c_void_p)),
                "rtg_context_scene_stats")

@@ -50,6 +50,7 @@ struct HostScene {
     memcpy(r.r2, g + 28, 4 * 4);
   }
   float first_lane(float v) const { return v; }
+  int first_lane_i(int v) const { return v; }
   rtg::V3 sphere(unsigned i, float& r2) const {
     const float* g = geom + 4 * i;
     r2 = g[3];

@@ -17,7 +17,7 @@ shift $((OPTIND - 1))
 for r in $(seq "$N"); do
   for L in "$@"; do
     RTG_LIB=$L timeout -k 10 200 python bench.py --config "$C" --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline \
-        --no-work-count --no-e2e 2>/dev/null \
+        --no-work-count --no-e2e 2>>gpurun_out/ab_bench.err \
       | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print('$C', '$(basename "$L")', d['kernel_ms'], d['parity'].get('bit_exact'), flush=True)" || exit 1
   done
 done
