@@ -718,8 +718,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
                   RTG_MAX_STACK, variant);
     return RTG_ERR_INVALID;
   }
-  const size_t frameLds =
-      (size_t)frame_lds_levels(stackSize, ctx->bvhNodes != nullptr) * threads * 16;
+  // the frame levels the chosen kernel keeps in LDS (its kBvh instantiation
+  // keeps one fewer, LdsFramesTop)
+  const bool bvhKernel = ctx->bvhNodes != nullptr && has_bvh_kernel(variant);
+  const size_t frameLds = (size_t)frame_lds_levels(stackSize, bvhKernel) * threads * 16;
   const size_t lds = frameLds +
                      (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) + (size_t)ctx->n4 * 16)
                               : 0) +

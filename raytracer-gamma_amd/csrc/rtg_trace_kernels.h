@@ -1016,7 +1016,13 @@ static TraceFn trace_fn_v(bool lds, int list) {
 }
 // BVH scenes: the default kernels (and their diagnostic and OpenCL-semantics
 // forms) have kBvh instantiations; other A/B variants run BVH scenes through
-// their flat queries (same results, slower).
+// their flat queries (same results, slower).  The launcher sizes a kBvh
+// kernel's LDS by frame_lds_levels(S, true), so this list and
+// has_bvh_kernel() must agree.
+inline bool has_bvh_kernel(int variant) {
+  return variant == 0 || variant == 50 || variant == 110 || variant == 120 || variant == 9 ||
+         variant == 59 || variant == 100;
+}
 template <int S>
 static TraceFn trace_fn_bvh(bool lds, int variant) {
   switch (variant) {
