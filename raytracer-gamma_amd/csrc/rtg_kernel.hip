@@ -233,6 +233,10 @@ struct rtg_context {
   unsigned* cone = nullptr;   // secondary-ray cone masks (null when none)
   float* prim = nullptr;      // primary-cull sphere constants
   float* bvhNodes = nullptr;  // BVH node records (null when the scene has none)
+  float* capRec = nullptr;    // sphere lists of BVH scenes (null when none)
+  unsigned* capOff = nullptr;
+  float* ovRec = nullptr;
+  unsigned* ovOff = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   unsigned long long* counts = nullptr;  // unit counters of the counting build (variant 120)
@@ -274,6 +278,14 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->prim);
   c->prim = nullptr;
   (void)hipFree(c->bvhNodes);
+  (void)hipFree(c->capRec);
+  (void)hipFree(c->capOff);
+  (void)hipFree(c->ovRec);
+  (void)hipFree(c->ovOff);
+  c->capRec = nullptr;
+  c->capOff = nullptr;
+  c->ovRec = nullptr;
+  c->ovOff = nullptr;
   c->smask = nullptr;
   c->bvhNodes = nullptr;
   c->geom = nullptr;
@@ -543,6 +555,24 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->bvhNodes, ps.bvhNodes.data(), ps.bvhNodes.size() * sizeof(float),
                       hipMemcpyHostToDevice));
   }
+  if (!ps.capOff.empty()) {
+    if (hipMalloc(&ctx->capRec, (ps.capRec.size() + kListWords) * sizeof(float)) != hipSuccess ||
+        hipMalloc(&ctx->capOff, ps.capOff.size() * sizeof(unsigned)) != hipSuccess ||
+        hipMalloc(&ctx->ovRec, (ps.ovRec.size() + kListWords) * sizeof(float)) != hipSuccess ||
+        hipMalloc(&ctx->ovOff, ps.ovOff.size() * sizeof(unsigned)) != hipSuccess) {
+      free_scene(ctx);
+      rtg_set_error("hipMalloc failed for the sphere lists");
+      return RTG_ERR_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(ctx->capRec, ps.capRec.data(), ps.capRec.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->capOff, ps.capOff.data(), ps.capOff.size() * sizeof(unsigned),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->ovRec, ps.ovRec.data(), ps.ovRec.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->ovOff, ps.ovOff.data(), ps.ovOff.size() * sizeof(unsigned),
+                      hipMemcpyHostToDevice));
+  }
   ctx->n = sphNum;
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
@@ -551,9 +581,12 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   ctx->sceneStats[0] = std::chrono::duration<double, std::milli>(tUp - tPack).count();
   ctx->sceneStats[1] = std::chrono::duration<double, std::milli>(tEnd - tUp).count();
   ctx->sceneStats[2] = (double)((ps.geom.size() + ps.crad2.size() + ps.mats.size() +
-                                 ps.lights.size() + ps.prim.size() + ps.bvhNodes.size()) *
+                                 ps.lights.size() + ps.prim.size() + ps.bvhNodes.size() +
+                                 ps.capRec.size() + ps.ovRec.size()) *
                                     sizeof(float) +
-                                (ps.smask.size() + ps.cone.size()) * sizeof(unsigned));
+                                (ps.smask.size() + ps.cone.size() + ps.capOff.size() +
+                                 ps.ovOff.size()) *
+                                    sizeof(unsigned));
   ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / kBvhWords);
   return RTG_OK;
 }
@@ -621,6 +654,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.cone = ctx->cone;
   a.prim = ctx->prim;
   a.bvhNodes = ctx->bvhNodes;
+  a.capRec = ctx->capRec;
+  a.capOff = ctx->capOff;
+  a.ovRec = ctx->ovRec;
+  a.ovOff = ctx->ovOff;
   a.n = ctx->n;
   a.m = ctx->m;
   a.n4 = ctx->n4;

@@ -16,6 +16,8 @@
 
 #include <algorithm>
 #include <functional>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "rtg.h"
@@ -54,6 +56,9 @@ struct PackedScene {
   // record of kBvhWords words per node (rtg_trace.h BvhRec, loaded with two
   // 64-byte scalar loads); empty for small or non-finite scenes.
   std::vector<float> bvhNodes;
+  // Sphere lists of BVH scenes (sphere_lists): capsule and overlap lists.
+  std::vector<float> capRec, ovRec;
+  std::vector<unsigned> capOff, ovOff;
   unsigned n = 0, m = 0;
   unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records + the fused part
 };
@@ -133,6 +138,56 @@ inline void prim_consts(const rtg_sphere& s, float* out) {
   out[2] = (float)sqrt(1.0 - sa * sa);
 }
 
+// The two mask predicates, shared by the masks (n <= 64) and the sphere lists
+// of BVH scenes (sphere_lists): sphere i can block a shadow ray from B_h to
+// light L (capsule_keep; *tOut = its centre's position along c_h -> L, 0..1),
+// and sphere j can contain a refraction test point of h / be hit by a ray that
+// entered h before it leaves B_h (overlap_keep).  See shadow_masks.
+inline bool capsule_keep(const rtg_sphere* spheres, unsigned h, unsigned i, const double L[3],
+                         double* tOut = nullptr) {
+  const rtg_sphere& sh = spheres[h];
+  const double A[3] = {sh.pos.x, sh.pos.y, sh.pos.z};
+  const double g = guard_radius(sh);
+  double ab[3], ab2 = 0.0;
+  for (int k = 0; k < 3; ++k) { ab[k] = L[k] - A[k]; ab2 += ab[k] * ab[k]; }
+  const double lh = sqrt(ab2);
+  const rtg_sphere& si = spheres[i];
+  const double C[3] = {si.pos.x, si.pos.y, si.pos.z};
+  const double ri = fabs((double)si.radius);
+  double t = 0.0, dch = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double ca = C[k] - A[k];
+    t += ca * ab[k];
+    dch += ca * ca;
+  }
+  dch = sqrt(dch);
+  t = ab2 > 0.0 ? t / ab2 : 0.0;
+  t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+  if (tOut) *tOut = (i == h) ? -1.0 : t;
+  if (i == h) return true;
+  double d2 = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double e = C[k] - (A[k] + t * ab[k]);
+    d2 += e * e;
+  }
+  const double mu = 0x1p-8 * (dch + g + ri) + 0x1p-16 * (lh + g);
+  const double reach = (g + ri + mu) * (1.0 + 1e-9);
+  return !(sqrt(d2) > reach);
+}
+inline bool overlap_keep(const rtg_sphere* spheres, unsigned h, unsigned j) {
+  if (j == h) return true;
+  const rtg_sphere& sh = spheres[h];
+  const double g = guard_radius(sh);
+  const double reach = contain_reach(sh);
+  const rtg_sphere& sj = spheres[j];
+  const double dx = (double)sj.pos.x - sh.pos.x, dy = (double)sj.pos.y - sh.pos.y,
+               dz = (double)sj.pos.z - sh.pos.z;
+  const double d = sqrt(dx * dx + dy * dy + dz * dz);
+  const double rj = fabs((double)sj.radius) + 1e-6;
+  const double mu = 0x1p-8 * (d + g + rj);
+  return !(d > (reach + rj + mu) * (1.0 + 1e-9));
+}
+
 inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
                          unsigned m, std::vector<unsigned>* out) {
   out->clear();
@@ -149,39 +204,9 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
   for (unsigned l = 0; l < m; ++l) {
     const double L[3] = {lights[l].pos.x, lights[l].pos.y, lights[l].pos.z};
     for (unsigned h = 0; h < n; ++h) {
-      const rtg_sphere& sh = spheres[h];
-      const double A[3] = {sh.pos.x, sh.pos.y, sh.pos.z};
-      const double g = guard_radius(sh);
-      double ab[3], ab2 = 0.0;
-      for (int k = 0; k < 3; ++k) { ab[k] = L[k] - A[k]; ab2 += ab[k] * ab[k]; }
-      const double lh = sqrt(ab2);
       unsigned* w = &(*out)[((size_t)l * n + h) * 2];
-      for (unsigned i = 0; i < n; ++i) {
-        bool keep = (i == h);
-        if (!keep) {
-          const rtg_sphere& si = spheres[i];
-          const double C[3] = {si.pos.x, si.pos.y, si.pos.z};
-          const double ri = fabs((double)si.radius);
-          double t = 0.0, dch = 0.0;
-          for (int k = 0; k < 3; ++k) {
-            const double ca = C[k] - A[k];
-            t += ca * ab[k];
-            dch += ca * ca;
-          }
-          dch = sqrt(dch);
-          t = ab2 > 0.0 ? t / ab2 : 0.0;
-          t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-          double d2 = 0.0;
-          for (int k = 0; k < 3; ++k) {
-            const double e = C[k] - (A[k] + t * ab[k]);
-            d2 += e * e;
-          }
-          const double mu = 0x1p-8 * (dch + g + ri) + 0x1p-16 * (lh + g);
-          const double reach = (g + ri + mu) * (1.0 + 1e-9);
-          keep = !(sqrt(d2) > reach);
-        }
-        if (keep) w[i >> 5] |= 1u << (i & 31);
-      }
+      for (unsigned i = 0; i < n; ++i)
+        if (capsule_keep(spheres, h, i, L)) w[i >> 5] |= 1u << (i & 31);
     }
   }
   // Overlap masks (closest_enter and primary_container_sel, rtg_trace.h): bit
@@ -199,21 +224,85 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
   //    point more than mu_j outside ball(c_j, |r_j| + 1e-6); so the first
   //    containing sphere in index order is the first containing mask sphere.
   for (unsigned h = 0; h < n; ++h) {
-    const rtg_sphere& sh = spheres[h];
-    const double g = guard_radius(sh);
-    const double reach = contain_reach(sh);
     unsigned* w = &(*out)[((size_t)m * n + h) * 2];
-    w[h >> 5] |= 1u << (h & 31);
-    for (unsigned j = 0; j < n; ++j) {
-      if (j == h) continue;
-      const rtg_sphere& sj = spheres[j];
-      const double dx = (double)sj.pos.x - sh.pos.x, dy = (double)sj.pos.y - sh.pos.y,
-                   dz = (double)sj.pos.z - sh.pos.z;
-      const double d = sqrt(dx * dx + dy * dy + dz * dz);
-      const double rj = fabs((double)sj.radius) + 1e-6;
-      const double mu = 0x1p-8 * (d + g + rj);
-      if (!(d > (reach + rj + mu) * (1.0 + 1e-9))) w[j >> 5] |= 1u << (j & 31);
+    for (unsigned j = 0; j < n; ++j)
+      if (overlap_keep(spheres, h, j)) w[j >> 5] |= 1u << (j & 31);
+  }
+}
+
+// Sphere lists of BVH scenes (n > 64, where 64-bit masks do not reach): the
+// masks' sets as lists of kListWords-word records, for the coherent-wave
+// queries of rtg_trace.h (blocked_cap, closest_enter_list, container_list):
+//  * capsule lists, one per (light l, sphere h): the spheres of shadow mask
+//    (l, h) (capsule_keep), nearest first along c_h -> L_l (h itself first),
+//    records {x, y, z, screen r^2 (screen_r2), r^2, 0, 0, 0};
+//  * overlap lists, one per sphere h: the spheres of overlap mask h
+//    (overlap_keep) in index order, records {x, y, z, screen r^2, r^2,
+//    (r + 1e-6f)^2, index, refractive index}.
+// capOff[l n + h] .. capOff[l n + h + 1] and ovOff[h] .. ovOff[h + 1] index
+// the records.  Empty for non-finite scenes (the queries then use the BVH).
+constexpr int kListWords = 8;
+inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
+                         unsigned m, PackedScene* ps) {
+  ps->capRec.clear();
+  ps->capOff.clear();
+  ps->ovRec.clear();
+  ps->ovOff.clear();
+  auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
+  for (unsigned i = 0; i < n; ++i)
+    if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
+        !finite(spheres[i].radius))
+      return;
+  for (unsigned l = 0; l < m; ++l)
+    if (!finite(lights[l].pos.x) || !finite(lights[l].pos.y) || !finite(lights[l].pos.z))
+      return;
+  auto rec = [&](std::vector<float>& v, unsigned i) {
+    const rtg_sphere& s = spheres[i];
+    const float r2 = s.radius * s.radius;  // raytracer.h:100
+    const float rc = s.radius + 1.0e-6f;   // raytracer.h:259-264
+    unsigned idx = i;
+    float fi;
+    memcpy(&fi, &idx, 4);
+    const float w[kListWords] = {s.pos.x, s.pos.y, s.pos.z, screen_r2(r2), r2, rc * rc, fi,
+                                 s.material.refractiveIndex};
+    v.insert(v.end(), w, w + kListWords);
+  };
+  // capsule lists: per (l, h) the kept spheres sorted by position along the
+  // capsule; the (l, h) pairs are independent, so they are built in parallel
+  std::vector<std::vector<unsigned>> lists((size_t)m * n);
+  auto work = [&](unsigned lo, unsigned hi) {
+    std::vector<std::pair<double, unsigned>> tmp;
+    for (unsigned q = lo; q < hi; ++q) {
+      const unsigned l = q / n, h = q % n;
+      const double L[3] = {lights[l].pos.x, lights[l].pos.y, lights[l].pos.z};
+      tmp.clear();
+      for (unsigned i = 0; i < n; ++i) {
+        double t;
+        if (capsule_keep(spheres, h, i, L, &t)) tmp.emplace_back(t, i);
+      }
+      std::sort(tmp.begin(), tmp.end());
+      for (const auto& e : tmp) lists[q].push_back(e.second);
     }
+  };
+  const unsigned total = m * n;
+  unsigned nt = std::thread::hardware_concurrency();
+  nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
+  if (total < 256) nt = 1;
+  std::vector<std::thread> pool;
+  for (unsigned t = 0; t < nt; ++t)
+    pool.emplace_back(work, (unsigned)((size_t)total * t / nt),
+                      (unsigned)((size_t)total * (t + 1) / nt));
+  for (auto& th : pool) th.join();
+  ps->capOff.push_back(0);
+  for (unsigned q = 0; q < total; ++q) {
+    for (unsigned i : lists[q]) rec(ps->capRec, i);
+    ps->capOff.push_back((unsigned)(ps->capRec.size() / kListWords));
+  }
+  ps->ovOff.push_back(0);
+  for (unsigned h = 0; h < n; ++h) {
+    for (unsigned j = 0; j < n; ++j)
+      if (overlap_keep(spheres, h, j)) rec(ps->ovRec, j);
+    ps->ovOff.push_back((unsigned)(ps->ovRec.size() / kListWords));
   }
 }
 
@@ -527,7 +616,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   shadow_masks(spheres, n, lights, m, &ps->smask);
   if (!ps->smask.empty()) cone_masks(spheres, n, &ps->cone);
   else ps->cone.clear();
-  build_bvh(spheres, n, ps);
+  if (build_bvh(spheres, n, ps)) sphere_lists(spheres, n, lights, m, ps);
   for (unsigned l = 0; l < m; ++l) {
     float* p = &ps->lights[(size_t)l * 6];
     p[0] = lights[l].pos.x; p[1] = lights[l].pos.y; p[2] = lights[l].pos.z;

@@ -224,6 +224,8 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kUUnwind,      // one unwind step (stage 1/2 colour sums)
              kUSample,      // one primary sample: ray set-up, cull hand-over, pixel sum
              kUBvhPass,     // (diagnostic) a BVH child-node screen passes for the lane
+             kUCapIter,     // blocked_cap: one capsule-list sphere (record, screen)
+             kUOvIter,      // closest_enter_list / container_list: one overlap-list sphere
              kUDiagShdSame,   // (diagnostic) shadow query, every lane on one hit sphere
              kUDiagEnterAll,  // (diagnostic) closest query, every lane's ray entered a sphere
              kUDiagEnterSame, // (diagnostic) ... the same sphere
@@ -549,6 +551,12 @@ template <int Q, class Scene>
 RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap);
 template <class Scene>
 RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel);
+template <class Scene>
+RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h);
+template <class Scene>
+RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT);
+template <class Scene>
+RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok);
 
 // raytracer.h:313-367, with the incidence test hoisted ahead of the shadow ray.
 // Q == 4: shadow rays test only the union of the wave's shadow masks
@@ -576,8 +584,11 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
           sc.count(kCntShadowQ, 1);
           sc.count(kCntShadowSel, __builtin_popcountll(su));
           blk = blocked_sel(sc, P, dir, gap, su);
+        } else if (sc.has_lists() && sc.all(guardOK) && sc.all(sc.first_lane_i(hit) == hit)) {
+          // BVH scene, coherent wave: sphere hit's capsule list for light l
+          sc.count(kUDiagShdSame, 1);
+          blk = blocked_cap(sc, P, dir, gap, l, sc.first_lane_i(hit));
         } else {
-          if (sc.has_bvh() && sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagShdSame, 1);
           blk = query_blocked<2>(sc, P, dir, gap);
         }
       } else {
@@ -704,8 +715,14 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
     sc.count(kCntContainSel, __builtin_popcountll(cu));
     tgt = primary_container_sel(sc, testPt, cu, nTgt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
+  } else if (hit >= 0 && sc.has_lists() &&
+             sc.all(guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax) &&
+             sc.all(sc.first_lane_i(hit) == hit)) {
+    // BVH scene, coherent wave: the first containing sphere of hit's overlap list
+    sc.count(kUDiagContSame, 1);
+    tgt = container_list(sc, testPt, sc.first_lane_i(hit), nTgt);
+    if (tgt < 0) tgt = (int)sc.n;  // background material
   } else {
-    if (sc.has_bvh() && sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagContSame, 1);
     sc.count(kCntContainFull, 1);
     tgt = primary_container(sc, testPt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
@@ -825,11 +842,17 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         sc.count(kCntFullQ, 1);
         hit = query_closest<2>(sc, o, d, t);
       }
+    } else if (Q == 4 && sc.has_lists() && sc.all(enterH >= 0) &&
+               sc.all(sc.first_lane_i(enterH) == enterH)) {
+      // BVH scene, coherent wave of rays that entered one sphere: it and its
+      // overlap list (closest_enter_list), else the BVH
+      sc.count(kUDiagEnterSame, 1);
+      bool ok;
+      sc.count(kUQuery, 1);
+      hit = closest_enter_list(sc, make_query(o, d), sc.first_lane_i(enterH), t, ok);
+      if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
     } else {
-      if (sc.has_bvh() && sc.all(enterH >= 0)) {
-        sc.count(kUDiagEnterAll, 1);
-        if (sc.all(sc.first_lane_i(enterH) == enterH)) sc.count(kUDiagEnterSame, 1);
-      }
+      if (sc.has_bvh() && sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
       sc.count(kCntFullQ, 1);
       hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
     }
@@ -1394,6 +1417,107 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
     }
   }
   return found == 0x7FFFFFFF ? -1 : found;
+}
+
+// ---------------------------------------------------------------------------
+// Coherent-wave queries of BVH scenes over the sphere lists (sphere_lists,
+// rtg_scene_pack.h): the n <= 64 masks' sets as lists, walked with a
+// wave-uniform index and one 32-byte scalar record load per sphere, no stack.
+// Taken when every active lane has the same sphere h (most waves of C5:
+// neighbouring samples hit the same sphere), else the BVH.
+
+// Shadow ray from a hit point P of sphere h (guard test passed) to light l:
+// only the spheres of h's capsule list can block it (shadow_masks' argument),
+// and the list is ordered nearest first, so blocked lanes stop early; the
+// wave leaves once every lane is blocked.  Same answer as blocked_bvh: any
+// blocker.
+template <class Scene>
+RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h) {
+  sc.count(kUQuery, 1);
+  const RayQ q = make_query(o, d);
+  unsigned k0, k1;
+  sc.cap_range(l, (unsigned)h, k0, k1);
+  bool blk = false;
+  for (unsigned k = k0; k < k1; ++k) {  // wave-uniform
+    sc.count(kUCapIter, 1);
+    float rs, r2, cr, rf;
+    int idx;
+    const V3 c = sc.cap_rec(k, rs, r2, cr, idx, rf);
+    if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
+      sc.count(kUShdExact, 1);
+      bool res;
+      const float t = ray_sphere(q, c, r2, res);
+      if (res && t < 1000.f) {
+        const V3 dist = vsmul(t, q.d);
+        if (vdot(dist, dist) < gap) blk = true;
+      }
+    }
+    if (sc.all(blk)) break;
+  }
+  return blk;
+}
+
+// Closest hit of rays that entered sphere h (every active lane): as
+// closest_enter_fused, with h's overlap list (index order) in place of the
+// mask; `ok` false for a lane whose origin or exit point leaves B_h (the
+// caller then runs the BVH query).  The winner is the lexicographic minimum of
+// (t, index), which is what the reference's index-order scan keeps.
+template <class Scene>
+RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok) {
+  sc.count(kUEnterHead, 1);
+  float r2h, g2;
+  const V3 ch = sc.sphere_guard(h, r2h, g2);
+  bool res;
+  const float th = ray_sphere(q, ch, r2h, res);
+  const V3 e0 = vsub(q.o, ch);
+  const V3 e1 = vsub(vadd(q.o, vsmul(th, q.d)), ch);
+  ok = res && th < 1000.f && vdot(e0, e0) <= g2 && vdot(e1, e1) <= g2;
+  tOut = 1000.f;
+  if (!sc.all(ok)) return -1;
+  float minT = th;
+  int best = h;
+  unsigned k0, k1;
+  sc.ov_range((unsigned)h, k0, k1);
+  for (unsigned k = k0; k < k1; ++k) {  // wave-uniform
+    float rs, r2, cr, rf;
+    int j;
+    const V3 c = sc.ov_rec(k, rs, r2, cr, j, rf);
+    if (j == h) continue;
+    sc.count(kUOvIter, 1);
+    if (!(pass1_rad(q, c, rs) < 0.f)) {
+      sc.count(kUEnterExact, 1);
+      bool rj;
+      const float t = ray_sphere(q, c, r2, rj);
+      if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
+    }
+  }
+  tOut = minT;
+  return best;
+}
+
+// primary_container (raytracer.h:245-270) for refraction test points of hits
+// on sphere h (every active lane; guard test passed, |D| <= kContainDirMax):
+// the first containing sphere of h's overlap list in index order (the
+// argument of primary_container_sel), and its refractive index in nT.
+template <class Scene>
+RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
+  int found = -1;
+  nT = sc.refr((int)sc.n);  // background material
+  unsigned k0, k1;
+  sc.ov_range((unsigned)h, k0, k1);
+  for (unsigned k = k0; k < k1; ++k) {  // wave-uniform
+    sc.count(kUOvIter, 1);
+    float rs, r2, cr, rf;
+    int j;
+    const V3 c = sc.ov_rec(k, rs, r2, cr, j, rf);
+    const V3 dist = vsub(pt, c);
+    if (found < 0 && vdot(dist, dist) <= cr) {
+      found = j;
+      nT = rf;
+    }
+    if (sc.all(found >= 0)) break;
+  }
+  return found;
 }
 
 template <class Scene>

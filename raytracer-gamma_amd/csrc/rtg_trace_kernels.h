@@ -184,6 +184,8 @@ struct DevScene {
   cfloat_p prim;  // n x {1/|c|, sin a, cos a, 0}: primary-cull sphere constants
   cfloat_p bvhNodes;  // BVH (build_bvh, rtg_scene_pack.h) or null
   int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
+  cfloat_p capRec, ovRec;  // sphere lists of BVH scenes (sphere_lists) or null
+  cuint_p capOff, ovOff;
   unsigned n, m;
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
@@ -235,6 +237,41 @@ struct DevScene {
     else return false;
   }
   __device__ __forceinline__ int* bvh_stack() const { return bvhStk; }
+  // Sphere lists (BVH scenes): ranges and 32-byte records (one scalar load).
+  __device__ __forceinline__ bool has_lists() const {
+    if constexpr (kBvh) return capOff != nullptr;
+    else return false;
+  }
+  __device__ __forceinline__ void cap_range(unsigned l, unsigned h, unsigned& k0,
+                                            unsigned& k1) const {
+    const cuint_p o = uidx(capOff, l * n + h);
+    k0 = o[0];
+    k1 = o[1];
+  }
+  __device__ __forceinline__ void ov_range(unsigned h, unsigned& k0, unsigned& k1) const {
+    const cuint_p o = uidx(ovOff, h);
+    k0 = o[0];
+    k1 = o[1];
+  }
+  __device__ __forceinline__ static V3 list_rec(cfloat_p base, unsigned k, float& rs, float& r2,
+                                                float& cr, int& idx, float& rf) {
+    typedef float f8 __attribute__((ext_vector_type(8)));
+    const f8 g = *(const RTG_CONST f8*)fidx(base, 8u * k);
+    rs = g[3];
+    r2 = g[4];
+    cr = g[5];
+    idx = __float_as_int(g[6]);
+    rf = g[7];
+    return v3(g[0], g[1], g[2]);
+  }
+  __device__ __forceinline__ V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
+                                        float& rf) const {
+    return list_rec(capRec, k, rs, r2, cr, idx, rf);
+  }
+  __device__ __forceinline__ V3 ov_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
+                                       float& rf) const {
+    return list_rec(ovRec, k, rs, r2, cr, idx, rf);
+  }
   // Node nd's record (BvhRec, rtg_trace.h): two 64-byte scalar loads.
   __device__ __forceinline__ void bvh_rec(unsigned nd, BvhRec& r) const {
     typedef float f16 __attribute__((ext_vector_type(16)));
@@ -431,6 +468,10 @@ struct KernelArgs {
   const unsigned* cone;   // cone masks (PackedScene::cone) or null
   const float* prim;      // primary-cull sphere constants (PackedScene::prim)
   const float* bvhNodes;  // BVH node records (PackedScene::bvhNodes) or null
+  const float* capRec;    // sphere lists (PackedScene::cap*, ov*) or null
+  const unsigned* capOff;
+  const float* ovRec;
+  const unsigned* ovOff;
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
@@ -536,6 +577,10 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.cone = (cuint_p)a.cone;
   sc.prim = (cfloat_p)a.prim;
   sc.bvhNodes = (cfloat_p)a.bvhNodes;
+  sc.capRec = (cfloat_p)a.capRec;
+  sc.capOff = (cuint_p)a.capOff;
+  sc.ovRec = (cfloat_p)a.ovRec;
+  sc.ovOff = (cuint_p)a.ovOff;
   // BVH scenes: 64 stack entries per wave after the frames and scene tables
   // (the launcher adds them to the LDS size).
   sc.bvhStk = reinterpret_cast<int*>(sceneLds + (kLds ? (a.n + 1) * 2 + a.n4 : 0)) +

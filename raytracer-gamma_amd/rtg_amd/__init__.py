@@ -76,7 +76,7 @@ UNIT_NAMES = [
     "U.bvhNode", "U.bvhSlot", "U.bvhExact", "U.contIter", "U.cont4", "U.contBvhNode", "U.cone",
     "U.maskIter", "U.node", "U.shade", "U.light", "U.shadow", "U.lit", "U.refr", "U.refrLeaf",
     "U.push", "U.descend", "U.unwind", "U.sample", "U.bvhPass",
-    "D.shdSame", "D.enterAll", "D.enterSame", "D.contSame",
+    "U.capIter", "U.ovIter", "D.shdSame", "D.enterAll", "D.enterSame", "D.contSame",
 ]
 
 

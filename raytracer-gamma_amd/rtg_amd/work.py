@@ -90,6 +90,10 @@ UNIT_COST = {
     "U.descend": 28,
     # colour sum (3), stage tests and frame update (9)
     "U.unwind": 12,
+    # sphere-list queries of BVH scenes (blocked_cap; closest_enter_list /
+    # container_list): one record's pass-1 screen (+ not-blocked) or containment test
+    "U.capIter": 13,
+    "U.ovIter": 13,
     # lane -> pixel / sample (6), sample_dir + vnorm (38), scaled sum, ordered
     # pixel sums (3 + 27), NaN canonicalisation and row bookkeeping (6)
     "U.sample": 80,

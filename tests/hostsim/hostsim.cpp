@@ -31,6 +31,35 @@ struct HostScene {
   bool any(bool b) const { return b; }
   int fuse = 0;  // fused query forms (rtg_trace.h kFuse*), set per variant
   const float* bvhNodes = nullptr;
+  const float* capRec = nullptr;
+  const unsigned* capOff = nullptr;
+  const float* ovRec = nullptr;
+  const unsigned* ovOff = nullptr;
+  bool has_lists() const { return capOff != nullptr; }
+  void cap_range(unsigned l, unsigned h, unsigned& k0, unsigned& k1) const {
+    k0 = capOff[l * n + h];
+    k1 = capOff[l * n + h + 1];
+  }
+  void ov_range(unsigned h, unsigned& k0, unsigned& k1) const {
+    k0 = ovOff[h];
+    k1 = ovOff[h + 1];
+  }
+  static rtg::V3 list_rec(const float* b, unsigned k, float& rs, float& r2, float& cr, int& idx,
+                          float& rf) {
+    const float* g = b + 8 * (size_t)k;
+    rs = g[3];
+    r2 = g[4];
+    cr = g[5];
+    memcpy(&idx, &g[6], 4);
+    rf = g[7];
+    return rtg::v3(g[0], g[1], g[2]);
+  }
+  rtg::V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
+    return list_rec(capRec, k, rs, r2, cr, idx, rf);
+  }
+  rtg::V3 ov_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
+    return list_rec(ovRec, k, rs, r2, cr, idx, rf);
+  }
   bool has_bvh() const { return bvhNodes != nullptr; }
   const float* prim = nullptr;
   const unsigned* cone = nullptr;
@@ -133,6 +162,7 @@ struct HostScene {
 
 int g_variant = 0;
 bool g_useBvh = true;
+bool g_useLists = true;  // the sphere lists of BVH scenes (coherent-wave queries)
 bool g_oldBoundScreen = false;  // hostsim_bvh_bound_check: the round-2 node screen
 double g_boundM = 0.0;          // hostsim_bvh_bound_check: margin m probe (0: kBoundM)
 
@@ -210,6 +240,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
+extern "C" void hostsim_use_lists(int on) { g_useLists = on != 0; }
 extern "C" void hostsim_old_bound_screen(int on) { g_oldBoundScreen = on != 0; }
 extern "C" void hostsim_bound_margin(double m) { g_boundM = m; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
@@ -240,6 +271,12 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
                 : 0;
   if (!ps.bvhNodes.empty() && g_useBvh) {
     sc.bvhNodes = ps.bvhNodes.data();
+    if (!ps.capOff.empty() && g_useLists) {
+      sc.capRec = ps.capRec.data();
+      sc.capOff = ps.capOff.data();
+      sc.ovRec = ps.ovRec.data();
+      sc.ovOff = ps.ovOff.data();
+    }
   }
   for (unsigned k = 0; k < nrows; ++k) {
     float* o = out + (size_t)k * W * 3;
