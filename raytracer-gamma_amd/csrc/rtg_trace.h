@@ -284,12 +284,14 @@ struct Frame {
 // property over 1e9 operand pairs (incl. subnormal numerators and values at
 // both thresholds) for den in [2^-60, 2^60].  Outside that range the correctly
 // rounded division is used.
-// BVH node screens (bound_screen / bound_r1, rtg_scene_pack.h build_bvh):
-// the line-distance margin m of a node bound, and the relative slack of the
-// screen's float evaluation.  RTG_BVH_OLD_SCREEN (A/B builds only): the
-// round-2 radicand screen with slack K_B = 2^-7 relative to |p|^2 + R^2.
+// BVH node screens (rtg_scene_pack.h build_bvh).  Default: pass1_bound, the
+// radicand screen with slack K_B = 2^-7 relative to |p_B|^2 + R^2.
+// RTG_BVH_OLD_SCREEN=0 (A/B builds): bound_screen / bound_r1, the
+// line-distance screen with margin m (|p_B| + R) — fewer node visits (-3 %
+// per ray on C5) but a square root and two more operations per slot: C5
+// 180.4-181.1 vs 177.0-177.2 ms on one box (profiles/r03/ab_c5_screen.log).
 #ifndef RTG_BVH_OLD_SCREEN
-#define RTG_BVH_OLD_SCREEN 0
+#define RTG_BVH_OLD_SCREEN 1
 #endif
 constexpr float kBoundK = 0x1p-7f;
 constexpr double kBoundM = 0x1p-8;               // m
@@ -1130,11 +1132,13 @@ inline float screen_r2(float r2) {
 // root's and the fused step's rounding), and the two a-terms scaled by
 // 1 -+ 2^-18 to cover the float evaluation's own error (< 20 eps a (|p_B|^2
 // + R_m^2)), so every line within R_m of C passes.  The slack is linear in
-// |p_B|: a node 40 units away keeps its radius within ~4 %, where the
-// round-2 screen (slack K_B a (|p_B|^2 + R^2), K_B = 2^-7, pass1_bound below)
-// let the bound grow by K_B |p_B|^2 / (2 R), several radii for a small far
-// node.  (tests/test_oracle.py::test_bvh_bounds_are_conservative checks it
-// on adversarial near-tangent and far, tiny spheres.)
+// |p_B|: a node 40 units away keeps its radius within ~4 %, where pass1_bound
+// (below, the default) lets the bound grow by K_B |p_B|^2 / (2 R), several
+// radii for a small far node; but its square root and two more operations
+// per slot cost more than the ~3 % of node visits it saves on C5, so it is
+// the A/B alternative (RTG_BVH_OLD_SCREEN=0).
+// (tests/test_oracle.py::test_bvh_bounds_are_conservative checks both on
+// adversarial near-tangent and far, tiny spheres.)
 RTG_HD float sqrt_hw(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_sqrtf(x);  // v_sqrt_f32, within 1 ulp
@@ -1160,8 +1164,12 @@ inline float bound_r1(double R) {
   return f;
 }
 
-// Round-2 node screen (RTG_BVH_OLD_SCREEN A/B builds): pass1_rad's with slack
-// K_B = kBoundK instead of K, i.e. K_B a (|p_B|^2 + R^2).
+// The default node screen (RTG_BVH_OLD_SCREEN): pass1_rad's with slack K_B =
+// kBoundK instead of K, i.e. K_B a (|p_B|^2 + R^2): a line the reference
+// accepts for member i passes within R + sqrt(15 eps) |p_i| of C (above), so
+// the bound's true radicand/4 is >= -2 sqrt(15 eps) a (|p_B|^2 + R^2) ~
+// -2^-9 a (...), which K_B = 2^-7 covers with room for the screen's own
+// rounding.
 RTG_HD float pass1_bound(const RayQ& q, V3 c, float rsB) {
   const V3 p = vsub(q.o, c);
   const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
