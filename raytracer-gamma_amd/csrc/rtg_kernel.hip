@@ -149,29 +149,38 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
 }
 
 // A block takes kCullGroups = 4 x 256 consecutive groups (one per lane per
-// round) and appends its live ones with ONE atomic: the atomics on the single
-// counter serialise in L2, so one per wave cost ~70 us on C3.
+// round) and appends its live ones with one atomic per class: the atomics on
+// the counters serialise in L2, so one per wave cost ~70 us on C3.
 constexpr unsigned kCullRounds = 4;
 // Each listed group's sphere mask goes to groupSel at the same list index:
 // the trace kernel takes it as the wave's primary-ray subset (one scalar
 // load) instead of recomputing the cull.
+// Heavy groups first (longest-processing-time order): the trace kernel's
+// waves take the list in order, and a launch ends with its last waves' tail
+// (a wave traces a whole pixel group; durations spread 3x around the
+// median), which dominates a short launch such as one GPU's shard of a
+// multi-GPU frame.  A group whose primary bundle can reach at least
+// a.lptMin spheres counts as heavy and is listed from the front
+// (groupCount[0]); the others are listed from the back of the array
+// (groupCount[1], index groupCap - 1 - k), and the trace kernel reads the
+// heavy run, then the light run in the order it was written.
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
                                                           unsigned long long* groupSel,
                                                           unsigned* groupCount) {
-  __shared__ unsigned cnt[kCullRounds][4];
-  __shared__ unsigned blockBase;
+  __shared__ unsigned cnt[2][kCullRounds][4];
+  __shared__ unsigned blockBase[2];
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned PPW = 64u / (nAA * nAA);
   const size_t total = (size_t)a.W * a.rowsLocal;
   const size_t blockG = (size_t)blockIdx.x * (256 * kCullRounds);
-  uint64_t live[kCullRounds], sel[kCullRounds];
+  uint64_t live[2][kCullRounds], sel[kCullRounds];
 #pragma unroll
   for (unsigned k = 0; k < kCullRounds; ++k) {
     const size_t g = blockG + k * 256 + threadIdx.x;
     sel[k] = g < nGroups ? group_sel(a, g, PPW, total) : 0ull;
-    const bool possible = sel[k] != 0ull;
+    const unsigned pc = (unsigned)__builtin_popcountll(sel[k]);
     // Zero-fill the pixels of all this wave's groups with coalesced stores
     // (the trace kernel, later on the same stream, overwrites the live ones).
     const size_t wg0 = g - lane;  // the wave's first group this round
@@ -181,31 +190,39 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
       if (q1 > total * 3) q1 = total * 3;
       for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
     }
-    live[k] = __ballot(possible);
-    if (lane == 0) cnt[k][wave] = (unsigned)__builtin_popcountll(live[k]);
+    live[0][k] = __ballot(pc >= a.lptMin);
+    live[1][k] = __ballot(pc != 0u && pc < a.lptMin);
+    if (lane == 0) {
+      cnt[0][k][wave] = (unsigned)__builtin_popcountll(live[0][k]);
+      cnt[1][k][wave] = (unsigned)__builtin_popcountll(live[1][k]);
+    }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 2) {
+    const unsigned c = threadIdx.x;
     unsigned sum = 0;
     for (unsigned k = 0; k < kCullRounds; ++k)
-      for (unsigned w = 0; w < 4; ++w) sum += cnt[k][w];
-    blockBase = sum ? atomicAdd(groupCount, sum) : 0u;
+      for (unsigned w = 0; w < 4; ++w) sum += cnt[c][k][w];
+    blockBase[c] = sum ? atomicAdd(&groupCount[c], sum) : 0u;
   }
   __syncthreads();
-  unsigned off = blockBase;  // list order: (round, wave, lane)
 #pragma unroll
-  for (unsigned k = 0; k < kCullRounds; ++k) {
-    for (unsigned w = 0; w < 4; ++w)
-      if (w < wave) off += cnt[k][w];
-    const uint64_t m = live[k];
-    if ((m >> lane) & 1ull) {
-      const unsigned at =
-          off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      groupList[at] = (unsigned)(blockG + k * 256 + threadIdx.x);
-      groupSel[at] = sel[k];
+  for (unsigned c = 0; c < 2; ++c) {
+    unsigned off = blockBase[c];  // list order: (round, wave, lane)
+#pragma unroll
+    for (unsigned k = 0; k < kCullRounds; ++k) {
+      for (unsigned w = 0; w < 4; ++w)
+        if (w < wave) off += cnt[c][k][w];
+      const uint64_t m = live[c][k];
+      if ((m >> lane) & 1ull) {
+        const unsigned r = off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        const unsigned at = c == 0 ? r : a.groupCap - 1u - r;
+        groupList[at] = (unsigned)(blockG + k * 256 + threadIdx.x);
+        groupSel[at] = sel[k];
+      }
+      for (unsigned w = wave; w < 4; ++w) off += cnt[c][k][w];
     }
-    for (unsigned w = wave; w < 4; ++w) off += cnt[k][w];
   }
 }
 
@@ -256,6 +273,7 @@ struct rtg_context {
   int nextSlot = 0;
   int numCU = 256;
   int persistPerCU = 0;  // > 0: fixed persistent waves per CU (RTG_PERSIST_PER_CU A/B knob)
+  int lptMin = 2;        // heavy-first listing threshold (cull_groups_kernel; RTG_LPT_MIN A/B knob)
   size_t timelineCap = 0, timelineCount = 0;
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
@@ -357,6 +375,10 @@ int rtg_context_create(int device, rtg_context** out) {
   if (const char* v = getenv("RTG_PERSIST_PER_CU")) {  // A/B knob (performance only)
     const int k = atoi(v);
     if (k >= 1 && k <= 4096) c->persistPerCU = k;
+  }
+  if (const char* v = getenv("RTG_LPT_MIN")) {  // A/B knob (performance only; 65 = off)
+    const int k = atoi(v);
+    if (k >= 1 && k <= 65) c->lptMin = k;
   }
   if (const char* v = getenv("RTG_VARIANT")) {  // A/B knob
     char* end = nullptr;
@@ -676,6 +698,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.groupList = nullptr;
   a.groupSel = nullptr;
   a.groupCount = nullptr;
+  a.groupCap = 0;
+  a.lptMin = (unsigned)ctx->lptMin;
   a.nPersist = 0;
   if (variant == 120) {  // executed-work counting build
     if (!ctx->counts) {
@@ -731,7 +755,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         HIP_TRY(hipMalloc(&slot->sel, groups * sizeof(unsigned long long)));
         slot->cap = groups;
       }
-      if (!slot->count) HIP_TRY(hipMalloc(&slot->count, sizeof(unsigned)));
+      if (!slot->count) HIP_TRY(hipMalloc(&slot->count, 2 * sizeof(unsigned)));
       cullGroups = groups;  // the cull pass is enqueued below, after the last failure point
       // about one wave per listed group: the benchmark scenes list 13-17 % of
       // their groups; a wave past the count exits at once, and a scene that
@@ -742,6 +766,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       a.groupList = slot->list;
       a.groupSel = slot->sel;
       a.groupCount = slot->count;
+      a.groupCap = (unsigned)groups;  // light groups are listed from index groups - 1 down
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
       grid = dim3(a.nPersist, 1);
     }
@@ -779,7 +804,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // so an error never leaves a cull pass (which zero-fills dst and fills the
   // slot's list) in flight without the slot's event behind it.
   if (slot) {
-    HIP_TRY(hipMemsetAsync(slot->count, 0, sizeof(unsigned), (hipStream_t)stream));
+    HIP_TRY(hipMemsetAsync(slot->count, 0, 2 * sizeof(unsigned), (hipStream_t)stream));
     hipLaunchKernelGGL(
         cull_groups_kernel,
         dim3((unsigned)((cullGroups + 256 * kCullRounds - 1) / (256 * kCullRounds))), dim3(256),

@@ -482,7 +482,9 @@ struct KernelArgs {
   // may hit, their count, and the number of persistent waves; null otherwise.
   const unsigned* groupList;
   const unsigned long long* groupSel;  // the listed groups' primary-ray sphere masks
-  const unsigned* groupCount;
+  const unsigned* groupCount;  // [0] heavy groups (listed from the front), [1] light (from the back)
+  unsigned groupCap;           // the list's length (light entries end at groupCap - 1)
+  unsigned lptMin;             // cull_groups_kernel's heavy threshold
   unsigned nPersist;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
   unsigned long long* counts;  // 2 x kCntSlots unit counters (counting build, variant 120)
@@ -910,11 +912,14 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
     const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
     // variant 24: the wave recomputes its primary cull (no cull-pass masks)
     const RTG_CONST unsigned long long* gsel = (const RTG_CONST unsigned long long*)a.groupSel;
-    const unsigned cnt = *(const RTG_CONST unsigned*)a.groupCount;
+    const unsigned nHeavy = ((const RTG_CONST unsigned*)a.groupCount)[0];
+    const unsigned cnt = nHeavy + ((const RTG_CONST unsigned*)a.groupCount)[1];
     for (unsigned idx = (unsigned)gw; idx < cnt; idx += a.nPersist) {
-      const unsigned g = __builtin_amdgcn_readfirstlane(list[idx]);
+      // heavy run from the front, then the light run from the back
+      const unsigned at = idx < nHeavy ? idx : a.groupCap - 1u - (idx - nHeavy);
+      const unsigned g = __builtin_amdgcn_readfirstlane(list[at]);
       trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(
-          a, sc, g, kVariant != 24, kVariant != 24 ? (uint64_t)gsel[idx] : 0ull);
+          a, sc, g, kVariant != 24, kVariant != 24 ? (uint64_t)gsel[at] : 0ull);
     }
   } else {
     constexpr int K = GroupsPerWave<kVariant>::value;

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--waves-per-block", type=int, default=4)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--shard", type=int, default=0)
+    ap.add_argument("--shards", type=int, default=1)
+    ap.add_argument("--row-block", type=int, default=8)
     a = ap.parse_args()
     import torch
     import rtg_amd as R
@@ -40,8 +43,12 @@ def main():
     ctx.set_variant(a.variant, ctx.LAUNCH_TIMELINE)
     out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     for _ in range(3):
-        ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=st)
+        ev[0].record()
+        ctx.render_device(W, H, out.data_ptr(), stack_size=S, row_block=a.row_block,
+                          shard=a.shard, n_shards=a.shards, stream=st)
+        ev[1].record()
     torch.cuda.synchronize()
     rec = ctx.diag_timeline().astype(np.int64)
     t0 = rec[:, 0]
@@ -71,8 +78,12 @@ def main():
     held_idle = (blk_end - t1[:nb * wpb].reshape(nb, wpb)).sum()
     # per-SIMD peak concurrency
     order = np.argsort(key, kind="stable")
+    # the last 10 % of the span: resident waves per SIMD (the tail)
+    tail = [float(((t0 <= t) & (t1 > t)).sum() / nsimd) for t in np.linspace(0.9 * span, span, 11)[:-1]]
     res = {
-        "config": a.config, "variant": a.variant, "waves": int(len(dur)),
+        "config": a.config, "variant": a.variant, "shard": [a.shard, a.shards, a.row_block],
+        "launch_ms_events": float(ev[0].elapsed_time(ev[1])), "waves": int(len(dur)),
+        "tail_last10pct_resident": [round(v, 2) for v in tail],
         "span_us": span / 100.0, "simds_seen": int(nsimd), "cus_seen": int(ncu),
         "mean_resident_waves_per_simd": float(mean_res),
         "occupancy_curve": [round(v, 2) for v in curve],
