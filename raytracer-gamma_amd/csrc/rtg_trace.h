@@ -293,6 +293,9 @@ struct Frame {
 #ifndef RTG_BVH_OLD_SCREEN
 #define RTG_BVH_OLD_SCREEN 1
 #endif
+#ifndef RTG_BVH_PREFETCH
+#define RTG_BVH_PREFETCH 0
+#endif
 constexpr float kBoundK = 0x1p-7f;
 constexpr double kBoundM = 0x1p-8;               // m
 constexpr float kBoundMK = 0x1.00004p-8f;        // m (1 + 2^-18)
@@ -1294,6 +1297,10 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active
                         BvhStack& st, Leaf&& leaf, bool shadowQ = false) {
   BvhRec r;
   sc.bvh_rec(nd, r);
+  // (RTG_BVH_PREFETCH A/B builds) touch the first cache line of every child
+  // node's record now, so that the next visit's loads hit the scalar cache;
+  // the loaded words are consumed only after this node's tests
+  const unsigned pf = RTG_BVH_PREFETCH ? sc.bvh_touch(r.ch) : 0u;
   int pc[4];
   float pk[4];
 #pragma unroll
@@ -1326,7 +1333,9 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active
       if (active && near && !(v < 0.f)) leaf((unsigned)~x, c, r.r2[k]);
     }
   }
-  return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
+  const int nx = push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
+  if (RTG_BVH_PREFETCH) sc.consume(pf);
+  return nx;
 }
 
 template <class Scene>

@@ -18,11 +18,15 @@ import sys
 
 from conftest import ROOT
 
-# the oracle-vs-reference and kernel-traversal tests (the slow full-frame and
-# million-pair bound checks stay in the normal, unsanitised run)
-SELECT = ("oracle_small_frames or oracle_edge or kernel_traversal_small_frames or "
-          "kernel_traversal_edge_cases or kernel_traversal_random_scenes or "
-          "opencl_semantics or oracle_vs_reference_random or kernel_traversal_bvh_random")
+# the oracle and kernel-traversal tests over every code path (flat, masked,
+# BVH and list queries, edge cases, the OpenCL semantics); the slow
+# full-frame, brute-force 1024-sphere and million-pair checks stay in the
+# normal, unsanitised run (the whole CPU suite should take minutes)
+SELECT = ("oracle_edge_cases or kernel_traversal_edge_cases or kernel_traversal_bvh_random or "
+          "(kernel_traversal_random_scenes and v0) or (kernel_traversal_random_scenes and v9) or "
+          "(oracle_small_frames and not c4 and not c5) or "
+          "(kernel_traversal_small_frames and v0 and not c5) or "
+          "(kernel_traversal_opencl_semantics)")
 
 
 def test_oracle_and_hostsim_under_asan_ubsan():
