@@ -293,8 +293,8 @@ struct Frame {
 #ifndef RTG_BVH_OLD_SCREEN
 #define RTG_BVH_OLD_SCREEN 1
 #endif
-#ifndef RTG_BVH_PREFETCH
-#define RTG_BVH_PREFETCH 0
+#ifndef RTG_FR0_REGS  // A/B builds: level 0's reflection child ray in VGPRs
+#define RTG_FR0_REGS 0
 #endif
 constexpr float kBoundK = 0x1p-7f;
 constexpr double kBoundM = 0x1p-8;               // m
@@ -792,6 +792,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
                        uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   FrameR fr[NF];                        // reflection child rays (private memory)
+  FrameR fr0;                           // RTG_FR0_REGS: level 0's, in VGPRs
   int sp = 0;                           // == level of the node being processed
   V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
@@ -927,9 +928,12 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             // calculateReflection, raytracer.h:817-842
             const float perp = 2.f * vdot(d, N);
             const V3 rd = vnorm(vsub(d, vsmul(perp, N)));
-            fr[lv].rd = rd;
-            fr[lv].ro = vadd(P, vsmul(0.01f, rd));
-            fr[lv].rI = rc;
+            FrameR r;
+            r.rd = rd;
+            r.ro = vadd(P, vsmul(0.01f, rd));
+            r.rI = rc;
+            if (RTG_FR0_REGS && lv == 0) fr0 = r;
+            else fr[lv] = r;
           }
           sc.count(kUDescend, 1);
           ++sp;
@@ -969,7 +973,16 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
         fc.set(lv, f);
-        o = fr[lv].ro; d = fr[lv].rd; I = fr[lv].rI; rm = (int)(f.meta >> 9);
+        FrameR r;
+        if (RTG_FR0_REGS && lv == 0) {
+          r = fr0;
+        } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+          if (RTG_FR0_REGS) asm volatile("" ::: "memory");  // no speculative scratch load
+#endif
+          r = fr[lv];
+        }
+        o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 9);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
         descend = true;
@@ -1297,10 +1310,6 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active
                         BvhStack& st, Leaf&& leaf, bool shadowQ = false) {
   BvhRec r;
   sc.bvh_rec(nd, r);
-  // (RTG_BVH_PREFETCH A/B builds) touch the first cache line of every child
-  // node's record now, so that the next visit's loads hit the scalar cache;
-  // the loaded words are consumed only after this node's tests
-  const unsigned pf = RTG_BVH_PREFETCH ? sc.bvh_touch(r.ch) : 0u;
   int pc[4];
   float pk[4];
 #pragma unroll
@@ -1333,9 +1342,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active
       if (active && near && !(v < 0.f)) leaf((unsigned)~x, c, r.r2[k]);
     }
   }
-  const int nx = push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
-  if (RTG_BVH_PREFETCH) sc.consume(pf);
-  return nx;
+  return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
 }
 
 template <class Scene>

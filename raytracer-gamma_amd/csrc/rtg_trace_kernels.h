@@ -272,16 +272,6 @@ struct DevScene {
                                        float& rf) const {
     return list_rec(ovRec, k, rs, r2, cr, idx, rf);
   }
-  // First word of each child node's record (scalar loads, XOR-folded): pulls
-  // those records' first cache lines into the scalar cache (RTG_BVH_PREFETCH).
-  __device__ __forceinline__ unsigned bvh_touch(const int* ch) const {
-    unsigned v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (ch[k] > 0) v ^= *(const RTG_CONST unsigned*)fidx(bvhNodes, kBvhWords * (unsigned)ch[k]);
-    return v;
-  }
-  __device__ __forceinline__ static void consume(unsigned v) { asm volatile("" ::"s"(v)); }
   // Node nd's record (BvhRec, rtg_trace.h): two 64-byte scalar loads.
   __device__ __forceinline__ void bvh_rec(unsigned nd, BvhRec& r) const {
     typedef float f16 __attribute__((ext_vector_type(16)));

@@ -71,8 +71,6 @@ struct HostScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   int* bvh_stack() const { return nullptr; }
-  unsigned bvh_touch(const int*) const { return 0u; }
-  static void consume(unsigned) {}
   void bvh_rec(unsigned nd, rtg::BvhRec& r) const {
     const float* g = bvhNodes + (size_t)rtg::kBvhWords * nd;
     memcpy(r.g, g, 16 * 4);
