@@ -199,8 +199,6 @@ def main():
     Rmax = rdist.padded_rows(H, B, world)
     my_rows = R.shard_rows(H, B, rank, world)
     shard = torch.zeros((Rmax, W, 3), dtype=torch.float32, device="cuda")
-    gathered = (torch.empty((world, Rmax, W, 3), dtype=torch.float32, device="cuda")
-                if (world > 1 and rank == 0) else None)
     frame_buf = (torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
                  if (world > 1 and rank == 0) else None)
     stream = torch.cuda.current_stream()
@@ -210,12 +208,22 @@ def main():
     # N > 1, rank 0: gather complete (after the waits) and assemble done
     ev_g = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    # N > 1: chunks of the padded shard (same row ranges on every rank); the
-    # global rows of this rank's real rows, for rtg_render_rows_device.
-    K = max(1, min(args.gather_chunks, Rmax)) if world > 1 else 1
-    bounds = [(Rmax * c) // K for c in range(K + 1)]
+    # N > 1: chunks of the padded shard, whole row blocks (same row ranges on
+    # every rank); chunk c's rows of all ranks are global rows [r0 G, r1 G),
+    # gathered into their own [world, r1 - r0] buffer and put in row order by
+    # the assemble kernel as soon as that chunk has arrived.  The global rows
+    # of this rank's real rows, for rtg_render_rows_device.
+    nblk = Rmax // B
+    K = max(1, min(args.gather_chunks, nblk)) if world > 1 else 1
+    bounds = [B * ((nblk * c) // K) for c in range(K + 1)]
+    gathered = ([torch.empty((world, bounds[c + 1] - bounds[c], W, 3), dtype=torch.float32,
+                             device="cuda") for c in range(K)]
+                if (world > 1 and rank == 0) else None)
     grow = torch.tensor(R.shard_row_indices(H, B, rank, world).astype(np.int64),
                         dtype=torch.int32, device="cuda") if world > 1 else None
+    # chunks render on two streams in turn, so one chunk's last waves overlap
+    # the next chunk's first ones (a launch ends with a tail of long waves)
+    rstreams = [torch.cuda.Stream(), torch.cuda.Stream()] if world > 1 else None
 
     frame = None
 
@@ -233,39 +241,50 @@ def main():
             return
         if i is not None:
             ev_k[i][0].record(stream)
+        for rs in rstreams:
+            rs.wait_stream(stream)
         works = []
         for c in range(K):
             r0, r1 = bounds[c], bounds[c + 1]
             nreal = max(0, min(r1, my_rows) - r0)
-            if nreal > 0:
-                ctx.render_rows_device(W, H, grow.data_ptr() + 4 * r0, nreal,
-                                       shard.data_ptr() + 12 * W * r0, stack_size=S, stream=sptr)
-            piece = shard[r0:r1]
-            if args.dist_backend == "nccl":  # RCCL gather over xGMI, overlapped
-                outs = [gathered[g, r0:r1] for g in range(world)] if rank == 0 else None
-                works.append(dist.gather(piece, outs, dst=0, async_op=True))
-            else:                            # rehearsal path through host memory
-                host = piece.cpu()
-                gl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
-                dist.gather(host, gl, dst=0)
-                if rank == 0:
-                    for g in range(world):
-                        gathered[g, r0:r1].copy_(gl[g])
+            rs = rstreams[c % 2]
+            with torch.cuda.stream(rs):
+                if nreal > 0:
+                    ctx.render_rows_device(W, H, grow.data_ptr() + 4 * r0, nreal,
+                                           shard.data_ptr() + 12 * W * r0, stack_size=S,
+                                           stream=rs.cuda_stream)
+                piece = shard[r0:r1]
+                if args.dist_backend == "nccl":  # RCCL gather over xGMI, overlapped
+                    outs = [gathered[c][g] for g in range(world)] if rank == 0 else None
+                    works.append(dist.gather(piece, outs, dst=0, async_op=True))
+                else:                            # rehearsal path through host memory
+                    host = piece.cpu()
+                    gl = [torch.empty_like(host) for _ in range(world)] if rank == 0 else None
+                    dist.gather(host, gl, dst=0)
+                    if rank == 0:
+                        for g in range(world):
+                            gathered[c][g].copy_(gl[g])
+                    works.append(None)
+        for rs in rstreams:
+            stream.wait_stream(rs)
         if i is not None:
             ev_k[i][1].record(stream)
-        for w in works:
-            w.wait()
-        if i is not None:
-            ev_g[i].record(stream)
-        if rank == 0:
-            if args.dist_backend == "nccl":  # native permute kernel on the device
-                ctx.assemble_shards_device(gathered.data_ptr(), world, Rmax, W, H, B,
-                                           frame_buf.data_ptr(), stream=sptr)
-                frame = frame_buf
-            else:
-                frame = rdist.assemble(gathered, H, B).contiguous()
+        for c in range(K):
+            if works[c] is not None:
+                works[c].wait()  # the current stream waits for chunk c's gather
+            if i is not None and c == K - 1:
+                ev_g[i].record(stream)
+            if rank == 0:  # chunk c in row order (native permute kernel), at global row r0 G
+                r0, r1 = bounds[c], bounds[c + 1]
+                hc = min(H - r0 * world, (r1 - r0) * world)
+                if hc > 0:
+                    ctx.assemble_shards_device(gathered[c].data_ptr(), world, r1 - r0, W, hc, B,
+                                               frame_buf.data_ptr() + 12 * W * r0 * world,
+                                               stream=sptr)
         if i is not None:
             ev_a[i].record(stream)
+        if rank == 0:
+            frame = frame_buf
 
     for _ in range(args.warmup):
         step()
@@ -305,9 +324,11 @@ def main():
                  "gather_tail_ms_rank0": round(gather_tail, 4),
                  "assemble_ms_rank0": round(assemble, 4),
                  "step_ms": round(elapsed / args.steps * 1e3, 4),
-                 "note": "render = this rank's shard chunks (HIP events); gather tail = end of "
-                         "rank 0's render to the last gathered chunk on its stream (the gathers "
-                         "of earlier chunks overlap rendering); assemble = row-order restore "
+                 "gather_chunks": K,
+                 "note": "render = this rank's shard chunks (HIP events, chunks on two "
+                         "streams in turn); gather tail = end of rank 0's render to the last "
+                         "gathered chunk on its stream (earlier chunks' gathers and assembles "
+                         "overlap rendering); assemble = the last chunk's row-order restore "
                          "on rank 0; step = wall time per frame, max over ranks"}
     else:
         kern_max_ms = kern_ms
