@@ -36,4 +36,12 @@ echo "== shard balance" &&
 timeout -k 10 600 python tools/shard_balance.py --config c4 --blocks 8,16 --json $OUT/shard_balance_c4.json > $OUT/shard_balance_c4.log 2>&1 &&
 timeout -k 10 600 python tools/shard_balance.py --config c3 --blocks 4,8 --json $OUT/shard_balance_c3.json > $OUT/shard_balance_c3.log 2>&1 &&
 tail -3 $OUT/shard_balance_c3.log &&
-echo "== done"
+echo "== profiles done" || exit 1
+echo "== PMC c5" &&
+TAG=${TAG}_c5 ARGS="--config c5 --steps 1 --warmup 1 --no-cpu-baseline --no-work-count --no-e2e" bash tools/gpu_pmc.sh > $OUT/pmc_c5.log 2>&1 && tail -6 $OUT/pmc_c5.log &&
+echo "== 2-rank rehearsal (gloo gather, both ranks on this GPU)" &&
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+    bench.py --gpus 2 --steps 5 --warmup 1 --dist-backend gloo > $OUT/bench2_gloo.json 2> $OUT/bench2_gloo.err &&
+echo "== timeline c3" &&
+timeout -k 10 300 python tools/timeline.py --config c3 --waves-per-block 1 --json $OUT/timeline_c3.json > /dev/null &&
+echo "== all done"
