@@ -5,7 +5,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out
 TAG=${TAG:-r01}
-ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-work-count --no-e2e"}
+CFG=${CFG:-c3}
+ARGS=${ARGS:-"--config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-work-count --no-e2e"}
 mkdir -p $OUT/pmc_$TAG
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $OUT/pmc_$TAG/counters_list.txt 2>&1 || true
@@ -19,4 +20,4 @@ for grp in "${GRPS[@]}"; do
      -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/pmc_$TAG/p$i.json 2> $OUT/pmc_$TAG/p$i.err || { echo "pass $i failed"; tail -5 $OUT/pmc_$TAG/p$i.err; exit 1; }
 done
 echo "== done"
-python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT/pmc_$TAG --json $OUT/pmc_$TAG/pmc_c3.json > $OUT/pmc_$TAG/summary.txt && cat $OUT/pmc_$TAG/summary.txt
+python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT/pmc_$TAG --config $CFG --json $OUT/pmc_$TAG/pmc_$CFG.json > $OUT/pmc_$TAG/summary.txt && cat $OUT/pmc_$TAG/summary.txt

@@ -38,7 +38,7 @@ timeout -k 10 600 python tools/shard_balance.py --config c3 --blocks 4,8 --json 
 tail -3 $OUT/shard_balance_c3.log &&
 echo "== profiles done" || exit 1
 echo "== PMC c5" &&
-TAG=${TAG}_c5 ARGS="--config c5 --steps 1 --warmup 1 --no-cpu-baseline --no-work-count --no-e2e" bash tools/gpu_pmc.sh > $OUT/pmc_c5.log 2>&1 && tail -6 $OUT/pmc_c5.log &&
+TAG=${TAG}_c5 CFG=c5 ARGS="--config c5 --steps 1 --warmup 1 --no-cpu-baseline --no-work-count --no-e2e" bash tools/gpu_pmc.sh > $OUT/pmc_c5.log 2>&1 && tail -6 $OUT/pmc_c5.log &&
 echo "== 2-rank rehearsal (gloo gather, both ranks on this GPU)" &&
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
     bench.py --gpus 2 --steps 5 --warmup 1 --dist-backend gloo > $OUT/bench2_gloo.json 2> $OUT/bench2_gloo.err &&
