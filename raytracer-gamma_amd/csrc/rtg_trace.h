@@ -296,6 +296,13 @@ struct Frame {
 #ifndef RTG_FR0_REGS  // A/B builds: level 0's reflection child ray in VGPRs
 #define RTG_FR0_REGS 0
 #endif
+// Probe builds only (RTG_SCRATCH_X2=1): every reflection child ray is also
+// written to a second private array and read back at unwind, doubling the
+// scratch traffic without changing any result — an A/B against the default
+// prices that traffic.
+#ifndef RTG_SCRATCH_X2
+#define RTG_SCRATCH_X2 0
+#endif
 constexpr float kBoundK = 0x1p-7f;
 constexpr double kBoundM = 0x1p-8;               // m
 constexpr float kBoundMK = 0x1.00004p-8f;        // m (1 + 2^-18)
@@ -793,6 +800,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   FrameR fr[NF];                        // reflection child rays (private memory)
   FrameR fr0;                           // RTG_FR0_REGS: level 0's, in VGPRs
+#if RTG_SCRATCH_X2
+  FrameR frx[NF];                       // probe: a second copy (scratch traffic x2)
+#endif
   int sp = 0;                           // == level of the node being processed
   V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
@@ -934,6 +944,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             r.rI = rc;
             if (RTG_FR0_REGS && lv == 0) fr0 = r;
             else fr[lv] = r;
+#if RTG_SCRATCH_X2
+            frx[lv] = r;
+#endif
           }
           sc.count(kUDescend, 1);
           ++sp;
@@ -982,6 +995,13 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
 #endif
           r = fr[lv];
         }
+#if RTG_SCRATCH_X2 && defined(__HIP_DEVICE_COMPILE__)
+        {
+          const FrameR rx = frx[lv];  // consumed by an empty asm: the load stays
+          asm volatile("" ::"v"(rx.ro.x), "v"(rx.ro.y), "v"(rx.ro.z), "v"(rx.rd.x), "v"(rx.rd.y),
+                       "v"(rx.rd.z), "v"(rx.rI.x), "v"(rx.rI.y), "v"(rx.rI.z));
+        }
+#endif
         o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 9);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
