@@ -391,21 +391,76 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
   }
 }
 
-// 4-wide BVH of bounding spheres (the queries are closest_bvh, blocked_bvh
-// and container_bvh in rtg_trace.h).  Top-down: a node's spheres are split in
-// two by a surface-area-style sweep (split below), and each half again, into
-// four groups; a group of one sphere becomes a sphere slot, a larger group a child
-// node; nodes of <= 4 spheres hold sphere slots only.  Bounds are computed in
-// double about the float-rounded centre C of the group's box:
-//   R  = max |c_i - C| + |r_i|            (screen: bound_r1(R), bound_screen)
-//   RC = (max |c_i - C| + |r_i| + 1e-6) (1 + 2^-16)   (containment, RC^2 up)
-//   prune radius R (1 + 2^-7), rounded up (|r_i| (1 + 2^-7) for a sphere
-//   slot; see beyond_t in rtg_trace.h).
-// Returns false (no BVH) for non-finite scenes or an implausibly deep tree.
+// 4-wide BVH of axis-aligned boxes (the queries are closest_bvh, blocked_bvh
+// and container_bvh in rtg_trace.h).  Each sphere gets a grown box (bvh_grow
+// below: every point the reference's root test can accept, and its
+// containment ball, lie inside with a margin for the kernel's slab
+// arithmetic); a node's slot holds the union of its spheres' grown boxes.
+// Top-down: a node's spheres are split in two by a surface-area sweep (split
+// below), and each half again, into four groups; a group of one sphere
+// becomes a sphere slot, a larger group a child node; nodes of <= 4 spheres
+// hold sphere slots only.  Returns false (no BVH) for non-finite scenes or an
+// implausibly deep tree.
 inline float round_up_f(double v) {
   float f = (float)v;
   if ((double)f < v) f = nextafterf(f, __builtin_inff());
   return f;
+}
+inline float round_down_f(double v) {
+  float f = (float)v;
+  if ((double)f > v) f = nextafterf(f, -__builtin_inff());
+  return f;
+}
+
+// The origin box B* of a scene: every ray origin the kernel queries — the
+// camera at 0 (main.cpp:417), hit points (within r_h + mu_h of their sphere,
+// mu_h = 2^-8 (|p| + |r_h|) <= 2^-8 (diam B* + r_max), rtg_trace.h) and the
+// reference's offsets P + 0.01 rd (|rd| ~ 1) — lies inside it:
+//   B* = box(0, c_i -+ |r_i|) grown by pad = 0.02 + 2^-6 (diagonal + r_max),
+// which exceeds 2^-8 (diam B* + r_max) + 0.0101 (diam B* <= diagonal +
+// 2 sqrt(3) pad).  `omax` is its largest coordinate magnitude.
+struct OriginBox {
+  double lo[3], hi[3], omax;
+};
+inline OriginBox origin_box(const rtg_sphere* spheres, unsigned n) {
+  OriginBox b;
+  double rmax = 0.0;
+  for (int a = 0; a < 3; ++a) b.lo[a] = b.hi[a] = 0.0;
+  for (unsigned i = 0; i < n; ++i) {
+    const double c[3] = {spheres[i].pos.x, spheres[i].pos.y, spheres[i].pos.z};
+    const double r = fabs((double)spheres[i].radius);
+    rmax = fmax(rmax, r);
+    for (int a = 0; a < 3; ++a) {
+      b.lo[a] = fmin(b.lo[a], c[a] - r);
+      b.hi[a] = fmax(b.hi[a], c[a] + r);
+    }
+  }
+  double d2 = 0.0;
+  for (int a = 0; a < 3; ++a) d2 += (b.hi[a] - b.lo[a]) * (b.hi[a] - b.lo[a]);
+  const double pad = 0.02 + 0x1p-6 * (sqrt(d2) + rmax);
+  b.omax = 0.0;
+  for (int a = 0; a < 3; ++a) {
+    b.lo[a] -= pad;
+    b.hi[a] += pad;
+    b.omax = fmax(b.omax, fmax(fabs(b.lo[a]), fabs(b.hi[a])));
+  }
+  return b;
+}
+
+// Sphere (c, r)'s grown box for rays whose origins lie within `pmax` of c
+// and have coordinates of magnitude <= omax (rtg_trace.h, "Why a box keeps
+// every sphere"): half-width |r| + 2^-8 (pmax + |r|) + 2^-18 (|c|_inf + |r| +
+// omax) + 2^-20, in double, rounded outward to float.  `m` is the 2^-8
+// margin (tests probe smaller ones).
+inline void bvh_grow(const double c[3], double r, double pmax, double omax, float lo[3],
+                     float hi[3], double m = 0x1p-8) {
+  r = fabs(r);
+  const double cm = fmax(fabs(c[0]), fmax(fabs(c[1]), fabs(c[2])));
+  const double w = r + m * (pmax + r) + 0x1p-18 * (cm + r + omax) + 0x1p-20;
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = round_down_f(c[a] - w);
+    hi[a] = round_up_f(c[a] + w);
+  }
 }
 
 inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
@@ -416,62 +471,58 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
         !finite(spheres[i].radius))
       return false;
+  const OriginBox ob = origin_box(spheres, n);
+  // grown boxes: 6 floats per sphere
+  std::vector<float> gb((size_t)n * 6);
+  for (unsigned i = 0; i < n; ++i) {
+    const double c[3] = {spheres[i].pos.x, spheres[i].pos.y, spheres[i].pos.z};
+    double p2 = 0.0;
+    for (int a = 0; a < 3; ++a) {
+      const double e = fmax(fabs(ob.lo[a] - c[a]), fabs(ob.hi[a] - c[a]));
+      p2 += e * e;
+    }
+    bvh_grow(c, spheres[i].radius, sqrt(p2), ob.omax, &gb[6 * (size_t)i], &gb[6 * (size_t)i + 3]);
+  }
   std::vector<unsigned> idx(n);
   for (unsigned i = 0; i < n; ++i) idx[i] = i;
   auto cen = [&](unsigned i, int ax) {
-    return ax == 0 ? (double)spheres[i].pos.x : ax == 1 ? (double)spheres[i].pos.y
-                                                        : (double)spheres[i].pos.z;
+    return 0.5 * ((double)gb[6 * (size_t)i + ax] + (double)gb[6 * (size_t)i + 3 + ax]);
   };
-  auto longest = [&](unsigned lo, unsigned hi) {
-    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
-    for (unsigned k = lo; k < hi; ++k)
-      for (int a = 0; a < 3; ++a) {
-        mn[a] = fmin(mn[a], cen(idx[k], a));
-        mx[a] = fmax(mx[a], cen(idx[k], a));
-      }
-    int ax = 0;
-    for (int a = 1; a < 3; ++a)
-      if (mx[a] - mn[a] > mx[ax] - mn[ax]) ax = a;
-    return ax;
+  auto grow = [&](unsigned i, double* mn, double* mx) {
+    for (int q = 0; q < 3; ++q) {
+      mn[q] = fmin(mn[q], (double)gb[6 * (size_t)i + q]);
+      mx[q] = fmax(mx[q], (double)gb[6 * (size_t)i + 3 + q]);
+    }
+  };
+  auto area = [](const double* mn, const double* mx) {
+    const double x = mx[0] - mn[0], y = mx[1] - mn[1], z = mx[2] - mn[2];
+    return x * y + y * z + z * x;
   };
   // Split of idx[lo, hi) (>= 2 spheres) into two non-empty runs, returned as
-  // the first index of the second run.  Sweeps the centroid order on each
-  // axis and minimises n_left * d_left^2 + n_right * d_right^2, d the half
-  // diagonal of a side's sphere box: the chance that a line passes a node's
-  // bounding sphere grows with its radius squared.
-  std::vector<double> sufD;
+  // the first index of the second run: the centroid order on each axis,
+  // minimising n_left * area_left + n_right * area_right (the chance that a
+  // line meets a box grows with its surface area).
+  std::vector<double> suf;
   auto split = [&](unsigned lo, unsigned hi) {
     const unsigned cnt = hi - lo;
     double bestCost = 1e308;
-    int bestAx = longest(lo, hi);
+    int bestAx = 0;
     unsigned bestK = cnt / 2;
-    sufD.assign(cnt + 1, 0.0);
+    suf.assign(cnt + 1, 0.0);
     for (int ax = 0; ax < 3; ++ax) {
       std::sort(idx.begin() + lo, idx.begin() + hi, [&](unsigned a, unsigned b) {
         const double ca = cen(a, ax), cb = cen(b, ax);
         return ca < cb || (ca == cb && a < b);
       });
-      auto box = [&](unsigned i, double* mn, double* mx) {
-        const double r = fabs((double)spheres[i].radius);
-        for (int q = 0; q < 3; ++q) {
-          mn[q] = fmin(mn[q], cen(i, q) - r);
-          mx[q] = fmax(mx[q], cen(i, q) + r);
-        }
-      };
-      auto diag2 = [](const double* mn, const double* mx) {
-        double d = 0.0;
-        for (int q = 0; q < 3; ++q) d += 0.25 * (mx[q] - mn[q]) * (mx[q] - mn[q]);
-        return d;
-      };
       double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
       for (unsigned k = cnt; k-- > 1;) {  // suffix boxes: runs [k, cnt)
-        box(idx[lo + k], mn, mx);
-        sufD[k] = diag2(mn, mx);
+        grow(idx[lo + k], mn, mx);
+        suf[k] = area(mn, mx);
       }
       double pmn[3] = {1e300, 1e300, 1e300}, pmx[3] = {-1e300, -1e300, -1e300};
       for (unsigned k = 1; k < cnt; ++k) {  // prefix [0, k) | suffix [k, cnt)
-        box(idx[lo + k - 1], pmn, pmx);
-        const double cost = k * diag2(pmn, pmx) + (cnt - k) * sufD[k];
+        grow(idx[lo + k - 1], pmn, pmx);
+        const double cost = k * area(pmn, pmx) + (cnt - k) * suf[k];
         if (cost < bestCost) {
           bestCost = cost;
           bestAx = ax;
@@ -485,27 +536,6 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     });
     return lo + bestK;
   };
-  // bound of idx[lo, hi): C (float), R, RC (double)
-  auto bound = [&](unsigned lo, unsigned hi, float C[3], double& R, double& RC) {
-    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
-    for (unsigned k = lo; k < hi; ++k) {
-      const rtg_sphere& s = spheres[idx[k]];
-      const double r = fabs((double)s.radius);
-      for (int a = 0; a < 3; ++a) {
-        mn[a] = fmin(mn[a], cen(idx[k], a) - r);
-        mx[a] = fmax(mx[a], cen(idx[k], a) + r);
-      }
-    }
-    for (int a = 0; a < 3; ++a) C[a] = (float)(0.5 * (mn[a] + mx[a]));
-    R = 0.0;
-    for (unsigned k = lo; k < hi; ++k) {
-      const rtg_sphere& s = spheres[idx[k]];
-      const double dx = cen(idx[k], 0) - C[0], dy = cen(idx[k], 1) - C[1],
-                   dz = cen(idx[k], 2) - C[2];
-      R = fmax(R, sqrt(dx * dx + dy * dy + dz * dz) + fabs((double)s.radius));
-    }
-    RC = (R + 1e-6) * (1.0 + 0x1p-16);
-  };
   int maxDepth = 0;
   // node for idx[lo, hi), returns its index
   std::function<int(unsigned, unsigned, int)> build = [&](unsigned lo, unsigned hi,
@@ -513,10 +543,10 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     maxDepth = depth > maxDepth ? depth : maxDepth;
     const int node = (int)(ps->bvhNodes.size() / kBvhWords);
     ps->bvhNodes.resize(ps->bvhNodes.size() + kBvhWords, 0.f);
-    {  // empty slots: NaN geometry, aux -1, child 0, r^2 0
+    {  // empty slots: NaN geometry, child 0
       float* e = &ps->bvhNodes[(size_t)node * kBvhWords];
-      for (int k = 0; k < 16; ++k) e[k] = __builtin_nanf("");
-      for (int k = 16; k < 24; ++k) e[k] = -1.f;
+      for (int k = 0; k < 24; ++k) e[k] = __builtin_nanf("");
+      for (int k = 28; k < 32; ++k) e[k] = -1.f;
     }
     unsigned g[5];
     const unsigned cnt = hi - lo;
@@ -534,31 +564,36 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
       const unsigned a = g[k], b = g[k + 1];
       if (a >= b) continue;
       int child;
-      float C[3], w, cr, rp, r2 = 0.f;
+      float s[6], cr = -1.f;
       if (b - a == 1) {
         const unsigned i = idx[a];
-        const rtg_sphere& s = spheres[i];
-        C[0] = s.pos.x; C[1] = s.pos.y; C[2] = s.pos.z;
-        r2 = s.radius * s.radius;  // raytracer.h:100, the leaf's exact root test
-        w = screen_r2(r2);
-        const float rc = s.radius + 1.0e-6f;
+        const rtg_sphere& sp = spheres[i];
+        s[0] = sp.pos.x; s[1] = sp.pos.y; s[2] = sp.pos.z;
+        const float r2 = sp.radius * sp.radius;  // raytracer.h:100, the exact root test
+        s[3] = screen_r2(r2);
+        s[4] = r2;
+        s[5] = round_up_f(fabs((double)sp.radius) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
+        const float rc = sp.radius + 1.0e-6f;  // raytracer.h:259-264
         cr = rc * rc;
-        rp = round_up_f(fabs((double)s.radius) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
         child = ~(int)i;
       } else {
-        double R, RC;
-        bound(a, b, C, R, RC);
-        w = RTG_BVH_OLD_SCREEN ? bound_r2(R * (1.0 + 0x1p-20)) : bound_r1(R);
-        cr = round_up_f(RC * RC);
-        rp = round_up_f(R * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));
+        float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+        float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+        for (unsigned t = a; t < b; ++t)
+          for (int q = 0; q < 3; ++q) {
+            mn[q] = fminf(mn[q], gb[6 * (size_t)idx[t] + q]);
+            mx[q] = fmaxf(mx[q], gb[6 * (size_t)idx[t] + 3 + q]);
+          }
+        for (int q = 0; q < 3; ++q) {
+          s[q] = mn[q];
+          s[3 + q] = mx[q];
+        }
         child = build(a, b, depth + 1);
       }
       float* rec = &ps->bvhNodes[(size_t)node * kBvhWords];
-      rec[4 * k + 0] = C[0]; rec[4 * k + 1] = C[1]; rec[4 * k + 2] = C[2]; rec[4 * k + 3] = w;
-      rec[16 + 2 * k] = rp;
-      rec[16 + 2 * k + 1] = cr;
+      for (int q = 0; q < 6; ++q) rec[6 * k + q] = s[q];
       memcpy(&rec[24 + k], &child, 4);
-      rec[28 + k] = r2;
+      rec[28 + k] = cr;
     }
     return node;
   };

@@ -284,15 +284,6 @@ struct Frame {
 // property over 1e9 operand pairs (incl. subnormal numerators and values at
 // both thresholds) for den in [2^-60, 2^60].  Outside that range the correctly
 // rounded division is used.
-// BVH node screens (rtg_scene_pack.h build_bvh).  Default: pass1_bound, the
-// radicand screen with slack K_B = 2^-7 relative to |p_B|^2 + R^2.
-// RTG_BVH_OLD_SCREEN=0 (A/B builds): bound_screen / bound_r1, the
-// line-distance screen with margin m (|p_B| + R) — fewer node visits (-3 %
-// per ray on C5) but a square root and two more operations per slot: C5
-// 180.4-181.1 vs 177.0-177.2 ms on one box (profiles/r03/ab_c5_screen.log).
-#ifndef RTG_BVH_OLD_SCREEN
-#define RTG_BVH_OLD_SCREEN 1
-#endif
 #ifndef RTG_FR0_REGS  // A/B builds: level 0's reflection child ray in VGPRs
 #define RTG_FR0_REGS 0
 #endif
@@ -303,17 +294,10 @@ struct Frame {
 #ifndef RTG_SCRATCH_X2
 #define RTG_SCRATCH_X2 0
 #endif
-constexpr float kBoundK = 0x1p-7f;
-constexpr double kBoundM = 0x1p-8;               // m
-constexpr float kBoundMK = 0x1.00004p-8f;        // m (1 + 2^-18)
-constexpr float kBoundSlack = 0x1p-18f;
-
 struct RayQ {
   V3 o, d;
   float a4, den, y;
   float ap;       // pass-1 screen: a (1 - K), K = 2^-16 (pass1_rad)
-  float apB;      // BVH bound screen (RTG_BVH_OLD_SCREEN): a (1 - K_B)
-  float bL, bH;   // BVH bound screen: a (1 -+ kBoundSlack)
   bool fast;
   bool slow;      // some active lane of the wave is not `fast` (wave-uniform)
 };
@@ -326,9 +310,6 @@ RTG_HD RayQ make_query(V3 o, V3 d) {
   q.a4 = 4.0f * a;
   q.den = 2.0f * a;
   q.ap = a * (1.0f - 0x1p-16f);
-  q.apB = a * (1.0f - kBoundK);
-  q.bL = a * (1.0f - kBoundSlack);
-  q.bH = a * (1.0f + kBoundSlack);
   q.fast = (q.den >= 0x1p-60f) && (q.den <= 0x1p60f);
   q.slow = any_lane(!q.fast);
   // y is used only when q.fast (quot, quot_k<true>); den is then in
@@ -1138,43 +1119,47 @@ inline float screen_r2(float r2) {
 
 // ---------------------------------------------------------------------------
 // BVH queries for scenes above 64 spheres (no shadow/overlap masks there).
-// The host builds a 4-wide tree of bounding spheres (build_bvh,
+// The host builds a 4-wide tree of axis-aligned boxes (build_bvh,
 // rtg_scene_pack.h); the wave walks it together: a node's child is visited
-// when the child's bound screen passes for ANY active lane (ballot), so node
-// indices, records and the stack stay wave-uniform (scalar loads, the stack
-// in one VGPR through v_writelane / v_readlane).  Leaf spheres get the
-// pass-1 screen and the reference's exact root test per lane.  The queries
-// take the same answers as the flat ones whatever order the tree visits
-// spheres in:
+// when the ray passes through the child's box for ANY active lane (ballot),
+// so node indices, records and the stack stay wave-uniform (scalar loads, the
+// stack in the wave's LDS).  Leaf spheres get the pass-1 screen and the
+// reference's exact root test per lane.  The queries take the same answers as
+// the flat ones whatever order the tree visits spheres in:
 //  * closest hit (raytracer.h:145-194: index order, strict <, minT from
 //    1000) = the lexicographic minimum of (t, i) over accepted roots t < 1000;
 //  * shadow (raytracer.h:272-309) = does ANY accepted root block;
 //  * container (raytracer.h:245-270) = the minimum index whose containment
 //    test passes.
-// A node bound (C, R) holds every member sphere (R >= |c_i - C| + |r_i|).
-// Which lines can the reference accept for member i?  Its radicand
-// (raytracer.h:95-104) carries a rounding error E <= ~60 eps a (|p_i|^2 +
-// r_i^2) (p_i = o - c_i: the subtraction, two dot products, the products and
-// the difference), so a computed radicand >= 0 implies a (r_i^2 - d_i^2) >=
-// -E/4 for the distance d_i from c_i to the line, i.e. d_i^2 <= r_i^2 + 15
-// eps (|p_i|^2 + r_i^2): d_i <= r_i (1 + 4 sqrt(eps)) + sqrt(15 eps) |p_i|
-// (sqrt(15 eps) ~ 9.5e-4; tests/test_oracle.py measures misses of up to
-// ~7e-4 |p| accepted).  With |p_i| <= |p_B| + R (p_B = o - C) the line passes
-// within
-//     R_m = R + m (|p_B| + R),   m = 2^-8 (four times that bound)
-// of C.  bound_screen tests exactly that, as a radicand: x^2 - a |p_B|^2 +
-// a R_m^2 >= 0 (x = d.p_B), with R_m from one hardware square root, R (1 + m)
-// rounded up on the host (bound_r1) and m inflated by 2^-18 (the square
-// root's and the fused step's rounding), and the two a-terms scaled by
-// 1 -+ 2^-18 to cover the float evaluation's own error (< 20 eps a (|p_B|^2
-// + R_m^2)), so every line within R_m of C passes.  The slack is linear in
-// |p_B|: a node 40 units away keeps its radius within ~4 %, where pass1_bound
-// (below, the default) lets the bound grow by K_B |p_B|^2 / (2 R), several
-// radii for a small far node; but its square root and two more operations
-// per slot cost more than the ~3 % of node visits it saves on C5, so it is
-// the A/B alternative (RTG_BVH_OLD_SCREEN=0).
-// (tests/test_oracle.py::test_bvh_bounds_are_conservative checks both on
-// adversarial near-tangent and far, tiny spheres.)
+//
+// Why a box keeps every sphere the reference accepts.  For an accepted root
+// t* of sphere i (raytracer.h:105-138) the exact point X = o + t* d lies
+// within r_i + mu_i of c_i, mu_i = 2^-8 (|p_i| + |r_i|), p_i = o - c_i: with
+// f(t) = |p_i + t d|^2 - r_i^2 the quadratic, |X - c_i|^2 - r_i^2 = f(t*),
+// and the radicand's rounding error E <= ~60 eps a (|p_i|^2 + r_i^2) bounds
+// f(t*) by ~2E / (4a) whether the exact line hits (root error near tangency)
+// or misses (a radicand >= 0 by rounding only), so |X - c_i| <= r_i +
+// sqrt(30 eps) (|p_i| + |r_i|), and 2^-8 is twice sqrt(30 eps).  Every ray
+// origin lies in the scene's origin box B* (the camera at 0 and hit points,
+// each within mu of its sphere, plus the reference's 0.01 offsets), so |p_i|
+// <= P_i, the distance from c_i to B*'s farthest corner; the builder grows
+// sphere i's box by e_i = 2^-8 (P_i + |r_i|) plus 2^-18 (|c_i| + |r_i| + O)
+// (O the largest coordinate of B*), the rounding of the slab test below
+// (3 eps (|box coordinate| + |o|) along each axis), and rounds it outward.
+// X is then inside every enclosing box with a margin that covers the slab
+// arithmetic, so each axis' computed entry <= t* <= its exit, hence tn <= t*
+// <= tf: the box passes when t* is within reach (t* <= minT for a closest
+// query; t* < sqrt(gap / a) for a shadow ray, |t* D|^2 < gap).
+// tests/test_oracle.py::test_bvh_bounds_are_conservative checks the box and
+// the sphere slots' prune on adversarial near-tangent / far / on-surface
+// rays, and that the check finds misses with a smaller margin.
+RTG_HD float rcp_hw(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);  // v_rcp_f32, within 1 ulp
+#else
+  return 1.0f / x;
+#endif
+}
 RTG_HD float sqrt_hw(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_sqrtf(x);  // v_sqrt_f32, within 1 ulp
@@ -1182,45 +1167,30 @@ RTG_HD float sqrt_hw(float x) {
   return sqrtf(x);
 #endif
 }
-RTG_HD float bound_screen_p(const RayQ& q, float xd, float p2, float R1) {
-  const float Rm = fmaf(sqrt_hw(p2), kBoundMK, R1);
-  return fmaf(xd, xd, fmaf(-q.bL, p2, q.bH * (Rm * Rm)));
-}
-RTG_HD float bound_screen(const RayQ& q, V3 c, float R1) {
-  const V3 p = vsub(q.o, c);
-  const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
-  const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-  return bound_screen_p(q, x, p2, R1);
-}
-// R (1 + m) (1 + 2^-20) rounded up to float, R given in double.
-inline float bound_r1(double R) {
-  const double v = R * (1.0 + kBoundM) * (1.0 + 0x1p-20);
-  float f = (float)v;
-  if ((double)f < v) f = nextafterf(f, __builtin_inff());
-  return f;
-}
 
-// The default node screen (RTG_BVH_OLD_SCREEN): pass1_rad's with slack K_B =
-// kBoundK instead of K, i.e. K_B a (|p_B|^2 + R^2): a line the reference
-// accepts for member i passes within R + sqrt(15 eps) |p_i| of C (above), so
-// the bound's true radicand/4 is >= -2 sqrt(15 eps) a (|p_B|^2 + R^2) ~
-// -2^-9 a (...), which K_B = 2^-7 covers with room for the screen's own
-// rounding.
-RTG_HD float pass1_bound(const RayQ& q, V3 c, float rsB) {
-  const V3 p = vsub(q.o, c);
-  const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
-  const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rsB)));
-  return fmaf(x, x, fmaf(-q.apB, cs, 0x1p-100f));
+// Per-query slab constants: inv = 1/d per axis (a component below 2^-64 in
+// magnitude taken as +2^-64: the line moves by < 2^-64 t, far inside the
+// box margin) and on = o * inv, so an axis' plane parameter is one fused
+// step, fma(plane, inv, -on).
+struct BoxQ {
+  V3 inv, on;
+};
+RTG_HD float slab_d(float v) { return fabsf(v) < 0x1p-64f ? 0x1p-64f : v; }  // NaN stays
+RTG_HD BoxQ make_boxq(const RayQ& q) {
+  BoxQ b;
+  b.inv = v3(rcp_hw(slab_d(q.d.x)), rcp_hw(slab_d(q.d.y)), rcp_hw(slab_d(q.d.z)));
+  b.on = v3(q.o.x * b.inv.x, q.o.y * b.inv.y, q.o.z * b.inv.z);
+  return b;
 }
-
-// Bound screen radius^2: R^2 (1 + 2 K_B + 4 K_B^2) >= R^2 (1 + K_B) / (1 - K_B),
-// R given in double, rounded up to float.
-inline float bound_r2(double R) {
-  const double K = (double)kBoundK;
-  const double v = R * R * (1.0 + 2.0 * K + 4.0 * K * K);
-  float f = (float)v;
-  if ((double)f < v) f = nextafterf(f, __builtin_inff());
-  return f;
+// Does the ray pass through box [lo, hi] at a parameter in [0, reach]?
+// (NaN rays pass: conservative.)
+RTG_HD bool slab_pass(const BoxQ& b, V3 lo, V3 hi, float reach, float& tn) {
+  const float x0 = fmaf(lo.x, b.inv.x, -b.on.x), x1 = fmaf(hi.x, b.inv.x, -b.on.x);
+  const float y0 = fmaf(lo.y, b.inv.y, -b.on.y), y1 = fmaf(hi.y, b.inv.y, -b.on.y);
+  const float z0 = fmaf(lo.z, b.inv.z, -b.on.z), z1 = fmaf(hi.z, b.inv.z, -b.on.z);
+  tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+  const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), reach));
+  return tn <= tf;
 }
 
 // Wave-uniform traversal stack: 64 entries of the wave's LDS area
@@ -1251,47 +1221,43 @@ struct BvhStack {
   RTG_HD bool empty() const { return sp == 0; }
 };
 
-// Distance pruning.  An accepted root t of sphere i (raytracer.h:105-138)
-// lies on the ray no nearer than |p_i| - r_i - mu_i with mu_i = 2^-8 (|p_i| +
-// r_i) (p_i = o - c_i; the same root-error bound as shadow_masks': roots
-// move by ~sqrt(14 eps)(|p| + r) near tangency), i.e. t |d| >= |p_i| - r_i -
-// mu_i; for a node bound (C, R) holding sphere i, |p_i| - r_i >= |p_B| - R
-// and mu_i <= 2^-8 (|p_B| + 2 R).  So with rp >= R (1 + 2^-7) (the slot's
-// prune radius) every member's accepted roots are beyond `reach` when
-//   |p_B| (1 - 2^-8) > rp + reach,
-// tested squared with p2 = |p_B|^2 (relative rounding below 2^-20 on both
+// Distance pruning of sphere slots.  An accepted root t of sphere i lies on
+// the ray no nearer than |p_i| - r_i - mu_i (mu_i above), i.e. t |d| >= |p_i|
+// - r_i - mu_i.  So with rp >= r_i (1 + 2^-7) (the slot's prune radius) its
+// accepted roots are beyond `reach` when
+//   |p_i| (1 - 2^-8) > rp + reach,
+// tested squared with p2 = |p_i|^2 (relative rounding below 2^-20 on both
 // sides, covered by the two factors).  `reach` is minT |d|_up for a closest
 // query (a root must be < minT, or == minT with a lower index, to win) and
 // sqrt(gap)_up for a shadow ray (|t D|^2 < gap to block).
-// tests/test_oracle.py::test_bvh_root_distance_bound checks the root bound
-// on adversarial rays.
+// tests/test_oracle.py::test_bvh_bounds_are_conservative checks the root
+// bound on adversarial rays.
 RTG_HD bool beyond(float p2, float rp, float reach) {
   const float s = rp + reach;
   return p2 * (0x1.fc02p-1f * (1.0f - 0x1p-18f)) > s * s * (1.0f + 0x1p-18f);
 }
 // |d| rounded up (v_sqrt_f32 is within 1 ulp).
-RTG_HD float norm_up(float a) { return sqrtf(a) * (1.0f + 0x1p-20f); }
+RTG_HD float norm_up(float a) { return sqrt_hw(a) * (1.0f + 0x1p-20f); }
 
 // BVH node record (build_bvh, rtg_scene_pack.h): kBvhWords words, read with
 // two 64-byte scalar loads at the top of a node visit, so the four slots'
 // tests run back to back on SGPR operands (no load latency per slot).
-//   g[4k..4k+3]  slot k: centre, w (bound_r1 for a child node, screen_r2 for
-//                a sphere)
-//   aux[2k]      prune radius rp, aux[2k+1] containment radius^2
-//   ch[k]        > 0 child node, < 0 ~sphere index, 0 empty
-//   r2[k]        a sphere slot's r*r (raytracer.h:100) for the exact test
+//   s[6k .. 6k+5]  slot k: a child node's box {lo.xyz, hi.xyz}, or a sphere's
+//                  {c.xyz, screen r^2 (screen_r2), r*r (raytracer.h:100),
+//                  prune radius rp}
+//   ch[k]          > 0 child node, < 0 ~sphere index, 0 empty
+//   cr[k]          a sphere slot's containment radius^2 (r + 1e-6f)^2
 constexpr int kBvhWords = 32;
 struct BvhRec {
-  float g[16];
-  float aux[8];
+  float s[24];
   int ch[4];
-  float r2[4];
+  float cr[4];
 };
 
 // Children of a node in front-to-back order for the wave: of the valid
-// (child, key) pairs, keys = a lane's |p_B|^2 (wave-uniform), the nearest is
-// returned (the next node: no stack round trip) and the others are pushed
-// farthest first.  Five compare-exchanges.
+// (child, key) pairs, keys = a lane's box entry parameter (wave-uniform), the
+// nearest is returned (the next node: no stack round trip) and the others are
+// pushed farthest first.  Five compare-exchanges.
 RTG_HD int push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2, float k2,
                        int c3, float k3) {
   auto cx = [](int& ca, float& ka, int& cb, float& kb) {
@@ -1319,15 +1285,16 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2,
   return nxt;
 }
 
-// One node of a ray query: bound screens and distance pruning of its four
-// slots; child nodes some active lane still needs are ordered front to back
-// (the nearest returned, the others pushed), sphere slots are handed to
-// `leaf(i, c, r2)` for lanes that pass the screen and the prune.  `active`:
-// the lane still queries; `reach`: its pruning reach.  Returns the next node
-// (> 0) or 0.
+// One node of a ray query: box tests of its child slots (reach `reachT` in
+// ray parameter units) and distance pruning + pass-1 screens of its sphere
+// slots (reach `reachD` in distance units); child nodes some active lane
+// still needs are ordered front to back (the nearest returned, the others
+// pushed), sphere slots are handed to `leaf(i, c, r2)` for lanes that pass.
+// `active`: the lane still queries.  Returns the next node (> 0) or 0.
 template <class Scene, class Leaf>
-RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active, float reach,
-                        BvhStack& st, Leaf&& leaf, bool shadowQ = false) {
+RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
+                        float reachT, float reachD, BvhStack& st, Leaf&& leaf,
+                        bool shadowQ = false) {
   BvhRec r;
   sc.bvh_rec(nd, r);
   int pc[4];
@@ -1339,27 +1306,25 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, unsigned nd, bool active
     const int x = r.ch[k];
     if (x == 0) continue;  // wave-uniform
     sc.count(kUBvhSlot, 1);
-    const V3 c = v3(r.g[4 * k], r.g[4 * k + 1], r.g[4 * k + 2]);
-    const float w = r.g[4 * k + 3];
-    const V3 p = vsub(q.o, c);
-    const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
-    const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-    const bool near = !beyond(p2, r.aux[2 * k], reach);
+    const float* g = &r.s[6 * k];
     if (x > 0) {
       sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
-      const float v = RTG_BVH_OLD_SCREEN
-                          ? fmaf(xd, xd, fmaf(-q.apB, p2 - w, 0x1p-100f))  // pass1_bound
-                          : bound_screen_p(q, xd, p2, w);
-      const bool pass = active && near && !(v < 0.f);
+      float tn;
+      const bool pass = active && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]),
+                                            reachT, tn);
       if (pass) sc.count(kUBvhPass, 1);
       if (sc.any(pass)) {
         pc[k] = x;
-        pk[k] = sc.first_lane(p2);
+        pk[k] = sc.first_lane(tn);
       }
     } else {
       sc.count(shadowQ ? kCntBvhShadowSphereTests : kCntBvhSphereTests, 1);
-      const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - w, 0x1p-100f));  // pass1_rad
-      if (active && near && !(v < 0.f)) leaf((unsigned)~x, c, r.r2[k]);
+      const V3 c = v3(g[0], g[1], g[2]);
+      const V3 p = vsub(q.o, c);
+      const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+      const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
+      const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - g[3], 0x1p-100f));  // pass1_rad
+      if (active && !beyond(p2, g[5], reachD) && !(v < 0.f)) leaf((unsigned)~x, c, g[4]);
     }
   }
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
@@ -1370,11 +1335,13 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
   float minT = 1000.f;
   int best = -1;
   const float dn = norm_up(q.den * 0.5f);
+  const BoxQ b = make_boxq(q);
   BvhStack st(sc.bvh_stack());
   unsigned nd = 0;  // the root
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
-    const int nx = bvh_ray_node(sc, q, nd, true, minT * dn, st, [&](unsigned i, V3 ce, float r2) {
+    const int nx = bvh_ray_node(sc, q, b, nd, true, minT, minT * dn, st,
+                                [&](unsigned i, V3 ce, float r2) {
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
@@ -1395,16 +1362,23 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
   return best;
 }
 
+// Shadow ray: blocked iff an accepted root t < 1000 has |t D|^2 < gap, so t
+// < sqrt(gap / a) (1 + 2^-18) covers the float test's rounding; a lane
+// outside the Markstein range (a tiny or huge) keeps the plain t < 1000.
 template <class Scene>
 RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   bool blk = false;
-  const float reach = norm_up(gap);
+  const float reachD = norm_up(gap);
+  float reachT = sqrt_hw(gap * rcp_hw(q.den * 0.5f)) * (1.0f + 0x1p-18f);
+  reachT = q.fast ? fminf(reachT, 1000.f) : 1000.f;
+  const BoxQ b = make_boxq(q);
   sc.count(kCntBvhShadowQ, 1);
   BvhStack st(sc.bvh_stack());
   unsigned nd = 0;  // the root
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
-    const int nx = bvh_ray_node(sc, q, nd, !blk, reach, st, [&](unsigned, V3 ce, float r2) {
+    const int nx = bvh_ray_node(sc, q, b, nd, !blk, reachT, reachD, st,
+                                [&](unsigned, V3 ce, float r2) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
@@ -1425,9 +1399,10 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   return blk;
 }
 
-// Node bounds for containment: |pt - C|^2 <= RC^2 with RC >= |c_i - C| +
-// |r_i| + 1e-6 and a relative 2^-16 margin (the reference's test accepts at
-// most a few ulps outside (r_i + 1e-6)); leaf slots hold (r_i + 1e-6f)^2.
+// Containment: a sphere's containment ball (r + 1e-6, raytracer.h:259-264,
+// which accepts at most a few ulps outside) lies inside its grown box, so a
+// point outside a child's box is in none of its spheres; sphere slots take
+// the reference's own test.
 template <class Scene>
 RTG_HD int container_bvh(const Scene& sc, V3 pt) {
   int found = 0x7FFFFFFF;
@@ -1442,15 +1417,17 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
     for (int k = 0; k < 4; ++k) {
       const int x = r.ch[k];
       if (x == 0) continue;
-      const V3 dist = vsub(pt, v3(r.g[4 * k], r.g[4 * k + 1], r.g[4 * k + 2]));
-      const bool in = vdot(dist, dist) <= r.aux[2 * k + 1];
+      const float* g = &r.s[6 * k];
       if (x > 0) {
+        const bool in = pt.x >= g[0] && pt.y >= g[1] && pt.z >= g[2] && pt.x <= g[3] &&
+                        pt.y <= g[4] && pt.z <= g[5];
         if (sc.any(in)) {  // the last such child is the next node, no stack round trip
           if (nxt > 0) st.push(nxt);
           nxt = x;
         }
-      } else if (in && (int)~x < found) {
-        found = (int)~x;
+      } else {
+        const V3 dist = vsub(pt, v3(g[0], g[1], g[2]));
+        if (vdot(dist, dist) <= r.cr[k] && (int)~x < found) found = (int)~x;
       }
     }
     if (nxt > 0) {

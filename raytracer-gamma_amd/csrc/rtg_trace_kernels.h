@@ -278,13 +278,13 @@ struct DevScene {
     const RTG_CONST f16* p = (const RTG_CONST f16*)fidx(bvhNodes, kBvhWords * nd);
     const f16 a = p[0], b = p[1];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) r.g[k] = a[k];
+    for (int k = 0; k < 16; ++k) r.s[k] = a[k];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) r.aux[k] = b[k];
+    for (int k = 0; k < 8; ++k) r.s[16 + k] = b[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       r.ch[k] = __float_as_int(b[8 + k]);
-      r.r2[k] = b[12 + k];
+      r.cr[k] = b[12 + k];
     }
   }
   // One lane's value for wave-uniform decisions (traversal order, cone cull).

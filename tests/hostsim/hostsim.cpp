@@ -73,10 +73,9 @@ struct HostScene {
   int* bvh_stack() const { return nullptr; }
   void bvh_rec(unsigned nd, rtg::BvhRec& r) const {
     const float* g = bvhNodes + (size_t)rtg::kBvhWords * nd;
-    memcpy(r.g, g, 16 * 4);
-    memcpy(r.aux, g + 16, 8 * 4);
+    memcpy(r.s, g, 24 * 4);
     memcpy(r.ch, g + 24, 4 * 4);
-    memcpy(r.r2, g + 28, 4 * 4);
+    memcpy(r.cr, g + 28, 4 * 4);
   }
   float first_lane(float v) const { return v; }
   int first_lane_i(int v) const { return v; }
@@ -163,8 +162,7 @@ struct HostScene {
 int g_variant = 0;
 bool g_useBvh = true;
 bool g_useLists = true;  // the sphere lists of BVH scenes (coherent-wave queries)
-bool g_oldBoundScreen = false;  // hostsim_bvh_bound_check: the round-2 node screen
-double g_boundM = 0.0;          // hostsim_bvh_bound_check: margin m probe (0: kBoundM)
+double g_boundM = 0.0;          // hostsim_bvh_bound_check: box margin probe (0: 2^-8)
 
 template <int S>
 void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, float* out) {
@@ -241,7 +239,6 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
 extern "C" void hostsim_use_lists(int on) { g_useLists = on != 0; }
-extern "C" void hostsim_old_bound_screen(int on) { g_oldBoundScreen = on != 0; }
 extern "C" void hostsim_bound_margin(double m) { g_boundM = m; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
 // the renders since the last reset (diagnostic; single-lane semantics, so the
@@ -604,9 +601,9 @@ extern "C" long hostsim_contain_mask_check(long scenes, unsigned n, long points,
 // BVH bounds against the reference's own root test (raytracer.h:81-141), on
 // adversarial ray/sphere pairs (near-tangent lines, far spheres, origins on
 // the surface, unnormalised directions, scales 1e-3..1e3):
-//  * bound screen (pass1_bound with K_B): for a node centre C at a random
-//    offset from the sphere and R = |c - C| + r (the tightest bound the
-//    builder makes), every accepted sphere passes;  -> *bad_screen
+//  * grown box (bvh_grow with the 2^-8 margin, origins within |o - c|):
+//    the kernel's slab test passes every accepted sphere's box within the
+//    closest query's reach t* and the shadow ray's reach;  -> *bad_screen
 //  * root distance (beyond): an accepted root t never lies nearer than
 //    |p| - r - 2^-8 (|p| + r) along the ray, so beyond() with reach just
 //    below t |d| never prunes it.  -> return value
@@ -680,41 +677,26 @@ extern "C" long hostsim_bvh_bound_check(long trials, unsigned long long seed, lo
     const float tr = rtg::ray_sphere(q, c, r2, res);
     if (!res) continue;
     ++acc;
-    // bound screen: node centre offset from c by up to 3 r (tightest R),
-    // mostly straight away from the line (the line's distance to C is then
-    // its distance to c plus the offset: the worst case)
-    double ox = u01() - 0.5, oy = u01() - 0.5, oz = u01() - 0.5;
-    if (t % 8 != 0) {
+    // grown box (bvh_grow) for origins within |o - c| of c: the ray passes
+    // through it within reach t* (a closest query's minT) and within a
+    // shadow ray's reach for the smallest gap that makes t* block
+    {
+      const double cd[3] = {c.x, c.y, c.z};
       const double px = (double)o.x - c.x, py = (double)o.y - c.y, pz = (double)o.z - c.z;
-      const double dd = (double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z;
-      const double s = -(px * d.x + py * d.y + pz * d.z) / dd;  // closest point o + s d
-      ox = -(px + s * d.x); oy = -(py + s * d.y); oz = -(pz + s * d.z);  // c - X
-    }
-    const double ol = sqrt(ox * ox + oy * oy + oz * oz) + 1e-300;
-    const double off = (t % 4 == 1) ? sqrt((double)rtg::vdot(rtg::vsub(o, c), rtg::vsub(o, c))) *
-                                          pow(10.0, -3.0 + 3.0 * u01())
-                                    : 3.0 * fabs((double)r) * u01();
-    const rtg::V3 C = rtg::v3((float)(c.x + off * ox / ol), (float)(c.y + off * oy / ol),
-                              (float)(c.z + off * oz / ol));
-    const double cx = (double)c.x - C.x, cy = (double)c.y - C.y, cz = (double)c.z - C.z;
-    const double R = sqrt(cx * cx + cy * cy + cz * cz) + fabs((double)r);
-    if (g_oldBoundScreen) {
-      const float w = rtg::bound_r2(R * (1.0 + 0x1p-20));
-      if (rtg::pass1_bound(q, C, w) < 0.f) ++badS;
-    } else {
-      // the kernel's screen with the device's square root, which may be 1 ulp
-      // low (the host's sqrtf rounds correctly): test with s (1 - 2^-23)
-      const rtg::V3 pB = rtg::vsub(o, C);
-      const float x = fmaf(d.x, pB.x, fmaf(d.y, pB.y, d.z * pB.z));
-      const float p2 = fmaf(pB.x, pB.x, fmaf(pB.y, pB.y, pB.z * pB.z));
-      float R1 = rtg::bound_r1(R), mK = rtg::kBoundMK;
-      if (g_boundM > 0.0) {  // margin probe: the same screen with another m
-        R1 = rtg::round_up_f(R * (1.0 + g_boundM) * (1.0 + 0x1p-20));
-        mK = (float)(g_boundM * (1.0 + 0x1p-18));
+      const double pm = sqrt(px * px + py * py + pz * pz) * (1.0 + 1e-12);
+      const double om = fmax(fabs((double)o.x), fmax(fabs((double)o.y), fabs((double)o.z)));
+      float lo[3], hi[3];
+      rtg::bvh_grow(cd, r, pm, om, lo, hi, g_boundM > 0.0 ? g_boundM : 0x1p-8);
+      const rtg::BoxQ bq = rtg::make_boxq(q);
+      float tn;
+      bool ok = rtg::slab_pass(bq, rtg::v3(lo[0], lo[1], lo[2]), rtg::v3(hi[0], hi[1], hi[2]), tr, tn);
+      const rtg::V3 dist = rtg::vsmul(tr, d);
+      const float gap = nextafterf(rtg::vdot(dist, dist), __builtin_inff());
+      if (ok && tr < 1000.f && q.fast) {
+        const float rt = fminf(sqrtf(gap * (1.0f / (q.den * 0.5f))) * (1.0f + 0x1p-18f), 1000.f);
+        ok = rtg::slab_pass(bq, rtg::v3(lo[0], lo[1], lo[2]), rtg::v3(hi[0], hi[1], hi[2]), rt, tn);
       }
-      const float Rm = fmaf(sqrtf(p2) * (1.0f - 0x1p-23f), mK, R1);
-      if (fmaf(x, x, fmaf(-q.bL, p2, q.bH * (Rm * Rm))) < 0.f) ++badS;
-      else if (g_boundM == 0.0 && rtg::bound_screen(q, C, R1) < 0.f) ++badS;
+      if (!ok) ++badS;
     }
     // root distance: reach = 0.999999 t |d| must not prune the sphere itself
     const float rp = rtg::round_up_f(fabs((double)r) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20));

@@ -346,14 +346,15 @@ def test_overlap_masks_bound_containment(hostsim):
 
 
 def test_bvh_bounds_are_conservative(hostsim):
-    """BVH node screens (bound_screen: every line within R + m (|p_B| + R) of
-    the node centre passes, m = 2^-8) keep every sphere the reference's root
-    test accepts, and the distance prune (beyond) never drops an accepted
-    root, over 3M adversarial near-tangent / far / on-surface ray-sphere pairs
-    at scales 1e-3..1e3 (rtg_trace.h closest_bvh).  The tiny-far-sphere cases
-    (lines the reference accepts although they miss by up to ~7e-4 |p|) need
-    m >= ~2^-10.5: at m = 2^-12 the same check finds misses.  The round-2
-    screen (pass1_bound, K_B = 2^-7; RTG_BVH_OLD_SCREEN builds) passes too."""
+    """BVH boxes (bvh_grow: half-width r + 2^-8 (|p| + r) + rounding terms)
+    pass the kernel's slab test for every sphere the reference's root test
+    accepts, within a closest query's reach t* and within the shadow ray's
+    reach sqrt(gap / a) for the smallest gap that makes t* block; and the
+    sphere slots' distance prune (beyond) never drops an accepted root, over
+    3M adversarial near-tangent / far / on-surface ray-sphere pairs at scales
+    1e-3..1e3 (rtg_trace.h closest_bvh / blocked_bvh).  The tiny-far-sphere
+    cases (lines the reference accepts although they miss by up to ~7e-4 |p|)
+    need a margin >= ~2^-10.5: at 2^-12 the same check finds misses."""
     f = hostsim.hostsim_bvh_bound_check
     f.restype = ctypes.c_long
     hostsim.hostsim_bound_margin.argtypes = [ctypes.c_double]
@@ -370,12 +371,8 @@ def test_bvh_bounds_are_conservative(hostsim):
     try:
         hostsim.hostsim_bound_margin(2.0 ** -12)
         assert run(1_000_000, 2027)[1] > 0  # the check has teeth
-        hostsim.hostsim_bound_margin(0.0)
-        hostsim.hostsim_old_bound_screen(1)
-        assert run(1_000_000, 2028)[:2] == (0, 0)
     finally:
         hostsim.hostsim_bound_margin(0.0)
-        hostsim.hostsim_old_bound_screen(0)
 
 
 def test_kernel_traversal_bvh_random_scenes(hostsim, oracle):
