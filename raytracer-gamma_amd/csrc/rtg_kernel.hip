@@ -774,19 +774,16 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // the compacted default kernel of a scene with shadow/overlap and cone masks
   // takes them as compile-time facts (kMasks)
   const int listKind = !listed ? 0 : (ctx->smask && ctx->cone) ? 2 : 1;
-  // BVH kernels keep 16-bit frame metas (LdsFramesTop): scenes above
-  // kBvhMaxSpheres run the flat queries
-  const bool bvhScene = ctx->bvhNodes != nullptr && ctx->n <= kBvhMaxSpheres;
-  TraceFn fn = pick_trace(stackSize, ldsMats, variant, bvhScene, listKind);
+  TraceFn fn = pick_trace(stackSize, ldsMats, variant, ctx->bvhNodes != nullptr, listKind);
   if (!fn) {
     rtg_set_error("no kernel for stackSize %d (valid: 1..%d), variant %d", stackSize,
                   RTG_MAX_STACK, variant);
     return RTG_ERR_INVALID;
   }
-  // the frame area of the chosen kernel (its kBvh instantiation keeps one
-  // level fewer, in 14 instead of 16 bytes per lane: LdsFramesTop)
-  const bool bvhKernel = bvhScene && has_bvh_kernel(variant);
-  const size_t frameLds = frame_lds_bytes(stackSize, bvhKernel, (int)threads);
+  // the frame levels the chosen kernel keeps in LDS (its kBvh instantiation
+  // keeps one fewer, LdsFramesTop)
+  const bool bvhKernel = ctx->bvhNodes != nullptr && has_bvh_kernel(variant);
+  const size_t frameLds = (size_t)frame_lds_levels(stackSize, bvhKernel) * threads * 16;
   const size_t lds = frameLds +
                      (ldsMats ? ((size_t)(ctx->n + 1) * 8 * sizeof(float) + (size_t)ctx->n4 * 16)
                               : 0) +

@@ -60,45 +60,23 @@ struct LdsFrames {
   __device__ __forceinline__ FrameC get(int lv) const { return base[lv * kThreads]; }
   __device__ __forceinline__ void set(int lv, const FrameC& v) const { base[lv * kThreads] = v; }
 };
-// BVH kernels (stack capacity >= 3): the deepest level `top` in four VGPRs
-// instead of LDS, and the LDS levels 0 .. top-1 split into a colour array
-// (12 B per lane: three conflict-free ds ops, the stride 3 words is odd) and a
-// 16-bit meta array, [level][thread] each: 14 B per lane and level instead of
-// 16, 2 KiB less LDS per wave at S = 8 (6 LDS levels + the traversal stack:
-// 5.5 KiB, so 7 waves per SIMD fit in 160 KiB; 16 B frames in every level
-// allowed 5).  The 16-bit meta is rm << 2 | flags: a BVH scene (n > 64) has
-// no cone masks, so FrameC::meta's origin-sphere bits are 0, and rm <= n <=
-// kBvhMaxSpheres (the launcher takes the flat kernel above that).  Level
-// `top` holds a frame only while a node of depth S - 1 (a leaf) is being
-// shaded below it.
-constexpr unsigned kBvhMaxSpheres = 16383;
+// The same with the deepest level `top` in four VGPRs instead of LDS (BVH
+// kernels, stack capacity >= 3): one KiB less LDS per wave, which is what
+// limits their occupancy (7 frame levels + the traversal stack at S = 8: 5
+// waves per SIMD; 6 with this).  Level `top` holds a frame only while a node
+// of depth S - 1 (a leaf) is being shaded below it.
 template <int kThreads>
 struct LdsFramesTop {
-  float* col;            // already offset by 3 * threadIdx.x; levels 0 .. top-1
-  unsigned short* meta;  // already offset by threadIdx.x
+  FrameC* base;  // already offset by threadIdx.x; levels 0 .. top-1
   int top;
   mutable FrameC reg;
   __device__ __forceinline__ FrameC get(int lv) const {
-    const int l = lv < top ? lv : top - 1;
-    const float* c = col + 3 * l * kThreads;
-    const unsigned m = meta[l * kThreads];
-    FrameC f;
-    f.cx = c[0];
-    f.cy = c[1];
-    f.cz = c[2];
-    f.meta = ((m >> 2) << 9) | (m & 3u);
-    return lv < top ? f : reg;
+    const FrameC l = base[(lv < top ? lv : top - 1) * kThreads];
+    return lv < top ? l : reg;
   }
   __device__ __forceinline__ void set(int lv, const FrameC& v) const {
-    if (lv < top) {
-      float* c = col + 3 * lv * kThreads;
-      c[0] = v.cx;
-      c[1] = v.cy;
-      c[2] = v.cz;
-      meta[lv * kThreads] = (unsigned short)(((v.meta >> 9) << 2) | (v.meta & 3u));
-    } else {
-      reg = v;
-    }
+    if (lv < top) base[lv * kThreads] = v;
+    else reg = v;
   }
 };
 
@@ -118,35 +96,15 @@ template <class MatPtr, bool kDiag = false, int kThreads = kBlock, bool kBvh = f
 struct DevScene {
   static constexpr int fuse = kFuse;
   static constexpr bool kIsBvh = kBvh;
-  FrameC* lfr;            // frames in LDS (LdsFrames), offset by threadIdx.x
-  float* lcol;            // BVH kernels (LdsFramesTop): colours, offset by 3 threadIdx.x
-  unsigned short* lmeta;  // BVH kernels: 16-bit metas, offset by threadIdx.x
+  FrameC* lfr;
   __device__ __forceinline__ bool all(bool b) const { return __ballot(!b) == 0ull; }
   __device__ __forceinline__ bool any(bool b) const { return __ballot(b) != 0ull; }
   // frame levels 0 .. nfl-1 in LDS (nfl = frame_lds_levels); BVH kernels keep
   // the deepest of NF levels in VGPRs (LdsFramesTop)
   int nfl;
   __device__ __forceinline__ auto frames() const {
-    if constexpr (kBvh) return LdsFramesTop<kThreads>{lcol, lmeta, nfl, FrameC{}};
+    if constexpr (kBvh) return LdsFramesTop<kThreads>{lfr, nfl, FrameC{}};
     else return LdsFrames<kThreads>{lfr};
-  }
-  // The pixel sum's parking slots (level 0 of the frame area, free once the
-  // trace is done): park this lane's sample, read lane k's (same wave).
-  __device__ __forceinline__ void park(V3 c) const {
-    if constexpr (kBvh) {
-      lcol[0] = c.x; lcol[1] = c.y; lcol[2] = c.z;
-    } else {
-      lfr->cx = c.x; lfr->cy = c.y; lfr->cz = c.z;
-    }
-  }
-  __device__ __forceinline__ V3 parked(unsigned k) const {
-    if constexpr (kBvh) {
-      const float* c = lcol + 3 * ((int)k - (int)(threadIdx.x & 63u));
-      return v3(c[0], c[1], c[2]);
-    } else {
-      const FrameC& f = lfr[(int)k - (int)(threadIdx.x & 63u)];
-      return v3(f.cx, f.cy, f.cz);
-    }
   }
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
   // probe slot, summed per wave and added to KernelArgs::diag at exit.
@@ -586,15 +544,10 @@ struct MinWaves {
 
 // Frame levels in LDS per lane: S - 1 ancestors (at least 1: the pixel sum
 // parks samples in level 0), one fewer for BVH kernels from S = 3 on
-// (LdsFramesTop keeps the deepest in VGPRs).  Bytes per lane and level: 16,
-// or 14 in BVH kernels (LdsFramesTop's split arrays).  launch_trace sizes
-// the LDS with frame_lds_bytes.
+// (LdsFramesTop keeps the deepest in VGPRs).  launch_trace sizes the LDS with
+// the same rule.
 constexpr int frame_lds_levels(int S, bool bvh) {
   return (S > 1 ? S - 1 : 1) - ((bvh && S >= 3) ? 1 : 0);
-}
-constexpr size_t frame_lds_bytes(int S, bool bvh, int threads) {
-  return bvh ? ((size_t)frame_lds_levels(S, true) * threads * 14 + 15) / 16 * 16
-             : (size_t)frame_lds_levels(S, false) * threads * 16;
 }
 
 // Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
@@ -602,15 +555,9 @@ template <int S, bool kLds, int kThreads, class Sc>
 __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   extern __shared__ float4 lds4[];
   constexpr int NFL = frame_lds_levels(S, Sc::kIsBvh);
+  sc.lfr = reinterpret_cast<FrameC*>(lds4) + threadIdx.x;
   sc.nfl = NFL;
-  if constexpr (Sc::kIsBvh) {
-    float* col = reinterpret_cast<float*>(lds4);
-    sc.lcol = col + 3 * threadIdx.x;
-    sc.lmeta = reinterpret_cast<unsigned short*>(col + 3 * NFL * kThreads) + threadIdx.x;
-  } else {
-    sc.lfr = reinterpret_cast<FrameC*>(lds4) + threadIdx.x;
-  }
-  float4* sceneLds = lds4 + frame_lds_bytes(S, Sc::kIsBvh, kThreads) / 16;
+  float4* sceneLds = lds4 + NFL * kThreads;
   if constexpr (kLds) {
     float* lmats = reinterpret_cast<float*>(sceneLds);
     const unsigned nm = (a.n + 1) * 8;
@@ -879,16 +826,19 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a0, Sc& sc, size_t
       pix.z = pix.z + __shfl(c.z, src);
     }
   } else {
-    sc.park(c);
+    FrameC* slot0 = sc.lfr - (threadIdx.x & 63u);  // this wave's level-0 slots
+    sc.lfr->cx = c.x;
+    sc.lfr->cy = c.y;
+    sc.lfr->cz = c.z;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (s == 0) {
       for (unsigned k = 0; k < SP; ++k) {
-        const V3 f = sc.parked((base + k) & 63u);
-        pix.x = pix.x + f.x;
-        pix.y = pix.y + f.y;
-        pix.z = pix.z + f.z;
+        const FrameC& f = slot0[(base + k) & 63u];
+        pix.x = pix.x + f.cx;
+        pix.y = pix.y + f.cy;
+        pix.z = pix.z + f.cz;
       }
     }
   }
@@ -1004,25 +954,6 @@ __global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_sgpr(RTG_NUM_SGPR)
 void trace_samples_kernel_masked(const KernelArgs a) {
   trace_samples_body<S, false, 0, false, true, true>(a);
 }
-
-// The BVH default kernel (S <= 8) built for 7 resident waves per SIMD: 5.5
-// KiB of LDS per wave at S = 8 (LdsFramesTop), at most 72 VGPRs, and an SGPR
-// budget that admits the seventh wave (the allocator's own count, 100+,
-// allows 6: tools/ubench/occ.hip).  RTG_BVH_WAVES=0 (A/B
-// builds) takes the unconstrained instantiation instead.
-#ifndef RTG_BVH_WAVES
-#define RTG_BVH_WAVES 7
-#endif
-#ifndef RTG_BVH_NUM_SGPR
-#define RTG_BVH_NUM_SGPR 94
-#endif
-#if RTG_BVH_WAVES > 0
-template <int S>
-__global__ __launch_bounds__(64, RTG_BVH_WAVES) __attribute__((amdgpu_num_sgpr(RTG_BVH_NUM_SGPR)))
-void trace_samples_kernel_bvh(const KernelArgs a) {
-  trace_samples_body<S, false, 0, true, false, false>(a);
-}
-#endif
 
 // Kernel variants (rtg_launch_opts.variant; results identical, speed differs):
 //   0 (default) sample-parallel: one primary sample per lane, one-wave
@@ -1145,11 +1076,7 @@ inline bool has_bvh_kernel(int variant) {
 template <int S>
 static TraceFn trace_fn_bvh(bool lds, int variant) {
   switch (variant) {
-    case 0:
-#if RTG_BVH_WAVES > 0
-      if constexpr (S <= 8) return trace_samples_kernel_bvh<S>;
-#endif
-      return trace_samples_kernel<S, false, 0, true>;
+    case 0: return trace_samples_kernel<S, false, 0, true>;
     case 50: return trace_samples_kernel<S, false, 50, true>;
     case 110: return trace_samples_kernel<S, false, 110, true>;
     case 120: return trace_samples_kernel<S, false, 120, true>;
