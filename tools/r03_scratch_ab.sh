@@ -11,7 +11,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-scratch_ab}
 mkdir -p $OUT
-LIBS="$PWD/ab/librtg_top.so $PWD/ab/librtg_fr0.so $PWD/ab/librtg_x2.so"
+LIBS=${LIBS:-"$PWD/ab/librtg_top.so $PWD/ab/librtg_fr0.so $PWD/ab/librtg_x2.so"}
 echo "== A/B c3" &&
 STEPS=20 bash tools/ab_bench.sh -r ${ROUNDS:-4} -c c3 $LIBS | tee $OUT/ab_c3.log &&
 echo "== A/B c4" &&
