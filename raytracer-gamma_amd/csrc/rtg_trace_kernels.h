@@ -664,13 +664,16 @@ __device__ __forceinline__ void trace_tile(const KernelArgs& a, Sc& sc, unsigned
 
 // Timeline record of one wave (launch flag RTG_LAUNCH_TIMELINE): start/end
 // s_memrealtime (100 MHz), HW_ID (hwreg 4) and XCC_ID (hwreg 20).  Called
-// with the wave converged.
-__device__ __forceinline__ void record_wave(const KernelArgs& a, unsigned t0, size_t w) {
+// with the wave converged.  `tag` (compacted launches) goes above XCC_ID's 4
+// bits: the popcount of the wave's first group's sphere mask (7 bits) and that
+// group's index (21 bits), for the launch-order analysis (tools/timeline.py).
+__device__ __forceinline__ void record_wave(const KernelArgs& a, unsigned t0, size_t w,
+                                            unsigned tag = 0) {
   if (a.timeline == nullptr) return;
   const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
-  if ((threadIdx.x & 63u) == 0) a.timeline[w] = make_uint4(t0, t1, hw, xcc);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
+  if ((threadIdx.x & 63u) == 0) a.timeline[w] = make_uint4(t0, t1, hw, xcc | (tag << 4));
 }
 
 // Tile kernels: one 8 x 8 pixel tile per wave, all samples of a pixel in its
@@ -908,6 +911,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
   // variant 21: kGroupsPerWave consecutive pixel groups per wave, in turn
   constexpr int Q = (kVariant == 15) ? 2 : 4;
   constexpr bool kDiag = IsDiag<kVariant>::value;
+  unsigned tag = 0;  // timeline tag (record_wave)
   if constexpr (kList) {
     const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
     // variant 24: the wave recomputes its primary cull (no cull-pass masks)
@@ -921,6 +925,12 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
       trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(
           a, sc, g, kVariant != 24, kVariant != 24 ? (uint64_t)gsel[at] : 0ull);
     }
+    if (a.timeline != nullptr && gw < cnt) {  // timeline tag: the wave's first group
+      const unsigned at = (unsigned)gw < nHeavy ? (unsigned)gw
+                                                : a.groupCap - 1u - ((unsigned)gw - nHeavy);
+      const unsigned g = list[at];
+      tag = ((unsigned)__builtin_popcountll(gsel[at]) & 127u) | ((g < 0x1FFFFFu ? g : 0x1FFFFFu) << 7);
+    }
   } else {
     constexpr int K = GroupsPerWave<kVariant>::value;
     for (int k = 0; k < K; ++k)
@@ -928,7 +938,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
                                                                                  gw * K + k);
   }
   if constexpr (kCount) sc.flush_counts(kargs()->counts);
-  record_wave(a, t0, gw);
+  record_wave(a, t0, gw, tag);
 }
 
 template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,

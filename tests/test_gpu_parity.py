@@ -397,6 +397,8 @@ def test_wave_timeline_diagnostic(R, golden, torch_cuda, variant):
         assert len(rec) == groups
     else:  # compacted launch: about one wave per listed group
         assert 0 < len(rec) <= groups
+        pc, grp = (rec[:, 3] >> 4) & 127, rec[:, 3] >> 11  # tag: first group's mask, index
+        assert pc.max() >= 1 and (pc <= c["spheres"]).all() and (grp < groups).all()
     dur = (rec[:, 1].astype(np.int64) - rec[:, 0].astype(np.int64)) % (1 << 32)
     assert (dur < 100_000_000).all()  # < 1 s each
     ctx.close()

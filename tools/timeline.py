@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--shards", type=int, default=1)
     ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--raw", default=None, help="also save the per-wave records (t0, t1 in "
+                    "10 ns ticks from the first start, hw id, xcc id; index = the wave's "
+                    "list position) to this .npz")
     a = ap.parse_args()
     import torch
     import rtg_amd as R
@@ -59,7 +62,12 @@ def main():
     t1 -= base
     span = t1.max()
     dur = t1 - t0
-    hw, xcc = rec[:, 2], rec[:, 3]
+    hw, xcc = rec[:, 2], rec[:, 3] & 15
+    tag = rec[:, 3] >> 4  # compacted launches: first group's mask popcount, group index
+    if a.raw:
+        np.savez_compressed(a.raw, t0=t0.astype(np.int32), t1=t1.astype(np.int32),
+                            hw=hw.astype(np.uint32), xcc=xcc.astype(np.uint8),
+                            popcount=(tag & 127).astype(np.uint8), group=(tag >> 7).astype(np.int32))
     simd = (hw >> 4) & 3
     cu = (hw >> 8) & 15
     sh = (hw >> 12) & 1
