@@ -46,9 +46,9 @@ extern "C" {
 #define RTG_ABI_VERSION 1
 #define RTG_MAX_STACK 16 /* largest supported RTSTACK_MAXSIZE */
 /* Scenes hold fewer than RTG_MAX_SPHERES spheres (rtg_context_set_scene
- * rejects larger ones with RTG_ERR_INVALID): the kernel keeps sphere and
- * material indices in 23-bit fields and 32-bit table offsets. */
-#define RTG_MAX_SPHERES (1u << 23)
+ * rejects larger ones with RTG_ERR_INVALID): the kernel keeps material
+ * indices in 22-bit fields and 32-bit table offsets. */
+#define RTG_MAX_SPHERES (1u << 22)
 
 /* vec.h:27-29 */
 typedef struct rtg_vec { float x, y, z; } rtg_vec;
@@ -217,8 +217,15 @@ int rtg_diag_read(rtg_context* ctx, unsigned long long* out8, int reset);
  * and returns n (cap <= 0: just returns n); negative on error. */
 int rtg_diag_counts(rtg_context* ctx, unsigned long long* out, int cap, int reset);
 #define RTG_LAUNCH_TIMELINE 1 /* record a per-wave timeline (rtg_diag_timeline) */
+/* Compacted launches list pixel groups heaviest first, by the trace times the
+ * previous launch of the same frame geometry measured (launch-order feedback:
+ * a scheduling hint, the frame is the same either way).  This flag lists them
+ * by primary-ray sphere count only (also env RTG_LAUNCH_ORDER=popcount). */
+#define RTG_LAUNCH_NO_ORDER_FEEDBACK 2
 /* Wave timeline of the last launch made with RTG_LAUNCH_TIMELINE: one record
- * per wave {start, end (s_memrealtime, 100 MHz, low 32 bits), HW_ID, XCC_ID},
+ * per wave {start, end (s_memrealtime, 100 MHz, low 32 bits), HW_ID, XCC_ID | tag << 4}
+ * (tag: the popcount of the wave's first group's sphere mask, 7 bits, then the
+ * group's index, 21 bits; compacted launches only),
  * in launch order.  Copies min(cap, waves) records; *count = waves recorded.
  * Diagnostic only (occupancy analysis, tools/timeline.py). */
 int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* count);

@@ -159,23 +159,35 @@ constexpr unsigned kCullRounds = 4;
 // waves take the list in order, and a launch ends with its last waves' tail
 // (a wave traces a whole pixel group; durations spread 3x around the
 // median), which dominates a short launch such as one GPU's shard of a
-// multi-GPU frame.  A group whose primary bundle can reach at least
-// a.lptMin spheres counts as heavy and is listed from the front
-// (groupCount[0]); the others are listed from the back of the array
-// (groupCount[1], index groupCap - 1 - k), and the trace kernel reads the
-// heavy run, then the light run in the order it was written.
+// multi-GPU frame.  The groups are listed in four runs, heaviest first
+// (KernelArgs::groupCount):
+//  * with launch-order feedback (a.costPrev: the previous launch of the same
+//    frame geometry measured every listed group's trace time, and its mean
+//    mu), by that time: >= 2 mu, >= mu, >= mu / 2, the rest.  A group's cost
+//    is a scheduling hint only: any value lists the group, so the frame is
+//    the same whatever the hint (a group dead last time reads a stale value);
+//  * otherwise (first launch) by the sphere mask: >= a.lptMin spheres first.
+// Run 0 fills the list's first half from the front, run 1 from its back,
+// runs 2 and 3 the second half likewise.
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
                                                           unsigned long long* groupSel,
                                                           unsigned* groupCount) {
-  __shared__ unsigned cnt[2][kCullRounds][4];
-  __shared__ unsigned blockBase[2];
+  __shared__ unsigned cnt[4][kCullRounds][4];
+  __shared__ unsigned blockBase[4];
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned PPW = 64u / (nAA * nAA);
   const size_t total = (size_t)a.W * a.rowsLocal;
   const size_t blockG = (size_t)blockIdx.x * (256 * kCullRounds);
-  uint64_t live[2][kCullRounds], sel[kCullRounds];
+  // the previous launch's mean group time (ticks), 0: no feedback
+  float mu = 0.f;
+  if (a.costPrev != nullptr) {
+    const unsigned long long st = *a.costPrev;
+    const unsigned ng = (unsigned)(st >> 40);
+    if (ng != 0u) mu = (float)(st & ((1ull << 40) - 1ull)) / (float)ng;
+  }
+  uint64_t live[4][kCullRounds], sel[kCullRounds];
 #pragma unroll
   for (unsigned k = 0; k < kCullRounds; ++k) {
     const size_t g = blockG + k * 256 + threadIdx.x;
@@ -190,15 +202,21 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
       if (q1 > total * 3) q1 = total * 3;
       for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
     }
-    live[0][k] = __ballot(pc >= a.lptMin);
-    live[1][k] = __ballot(pc != 0u && pc < a.lptMin);
-    if (lane == 0) {
-      cnt[0][k][wave] = (unsigned)__builtin_popcountll(live[0][k]);
-      cnt[1][k][wave] = (unsigned)__builtin_popcountll(live[1][k]);
+    unsigned run;
+    if (mu > 0.f) {
+      const float c = (pc != 0u) ? (float)a.groupCost[g] : 0.f;
+      run = c >= 2.f * mu ? 0u : c >= mu ? 1u : c >= 0.5f * mu ? 2u : 3u;
+    } else {
+      run = pc >= a.lptMin ? 0u : 1u;
+    }
+#pragma unroll
+    for (unsigned c = 0; c < 4; ++c) {
+      live[c][k] = __ballot(pc != 0u && run == c);
+      if (lane == 0) cnt[c][k][wave] = (unsigned)__builtin_popcountll(live[c][k]);
     }
   }
   __syncthreads();
-  if (threadIdx.x < 2) {
+  if (threadIdx.x < 4) {
     const unsigned c = threadIdx.x;
     unsigned sum = 0;
     for (unsigned k = 0; k < kCullRounds; ++k)
@@ -206,8 +224,9 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     blockBase[c] = sum ? atomicAdd(&groupCount[c], sum) : 0u;
   }
   __syncthreads();
+  const unsigned cap = a.groupCap;
 #pragma unroll
-  for (unsigned c = 0; c < 2; ++c) {
+  for (unsigned c = 0; c < 4; ++c) {
     unsigned off = blockBase[c];  // list order: (round, wave, lane)
 #pragma unroll
     for (unsigned k = 0; k < kCullRounds; ++k) {
@@ -217,7 +236,8 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
       if ((m >> lane) & 1ull) {
         const unsigned r = off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        const unsigned at = c == 0 ? r : a.groupCap - 1u - r;
+        const unsigned at = c == 0 ? r : c == 1 ? cap - 1u - r : c == 2 ? cap + r
+                                                                       : 2u * cap - 1u - r;
         groupList[at] = (unsigned)(blockG + k * 256 + threadIdx.x);
         groupSel[at] = sel[k];
       }
@@ -271,6 +291,24 @@ struct rtg_context {
   static constexpr int kSlots = 4;
   GroupSlot slots[kSlots];
   int nextSlot = 0;
+  // Launch-order feedback (cull_groups_kernel): per frame geometry, the
+  // groups' measured trace times of its last launch and the last two
+  // launches' sums; a few geometries at once (multi-GPU chunks render
+  // different row sets in turn), least recently used replaced.
+  struct CostEntry {
+    unsigned long long key = 0;
+    unsigned* cost = nullptr;
+    size_t cap = 0;
+    unsigned long long* stat = nullptr;  // [2]
+    int cur = 0;
+    unsigned launches = 0;
+    unsigned long long lastUse = 0;
+  };
+  static constexpr int kCostEntries = 8;
+  CostEntry costs[kCostEntries];
+  unsigned long long costClock = 0;
+  unsigned sceneGen = 0;  // bumped by rtg_context_set_scene (part of the geometry key)
+  bool orderFeedback = true;  // false: RTG_LAUNCH_ORDER=popcount (A/B knob)
   int numCU = 256;
   int persistPerCU = 0;  // > 0: fixed persistent waves per CU (RTG_PERSIST_PER_CU A/B knob)
   int lptMin = 2;        // heavy-first listing threshold (cull_groups_kernel; RTG_LPT_MIN A/B knob)
@@ -380,6 +418,9 @@ int rtg_context_create(int device, rtg_context** out) {
     const int k = atoi(v);
     if (k >= 1 && k <= 65) c->lptMin = k;
   }
+  if (const char* v = getenv("RTG_LAUNCH_ORDER")) {  // A/B knob (performance only)
+    if (strcmp(v, "popcount") == 0) c->orderFeedback = false;
+  }
   if (const char* v = getenv("RTG_VARIANT")) {  // A/B knob
     char* end = nullptr;
     const long var = strtol(v, &end, 10);
@@ -415,6 +456,10 @@ int rtg_context_destroy(rtg_context* ctx) {
     (void)hipFree(sl.sel);
     (void)hipFree(sl.count);
     if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  for (auto& ce : ctx->costs) {
+    (void)hipFree(ce.cost);
+    (void)hipFree(ce.stat);
   }
   delete ctx;
   return RTG_OK;
@@ -492,7 +537,7 @@ int rtg_set_launch_opts(rtg_context* ctx, const rtg_launch_opts* opts) {
     rtg_set_error("rtg_set_launch_opts: unknown kernel variant %d", opts->variant);
     return RTG_ERR_INVALID;
   }
-  if (opts->flags & ~RTG_LAUNCH_TIMELINE) {
+  if (opts->flags & ~(RTG_LAUNCH_TIMELINE | RTG_LAUNCH_NO_ORDER_FEEDBACK)) {
     rtg_set_error("rtg_set_launch_opts: unknown flags 0x%x", (unsigned)opts->flags);
     return RTG_ERR_INVALID;
   }
@@ -509,7 +554,7 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     return RTG_ERR_INVALID;
   }
   // Table limits of the kernel: a frame record keeps the refractive material
-  // index in 23 bits (FrameC::meta, rm << 9), and scene tables are addressed
+  // index in 22 bits (FrameC::meta, rm << 10), and scene tables are addressed
   // with 32-bit byte offsets (fidx / uidx; the fused records end at 80 n
   // bytes).  Both hold for n < RTG_MAX_SPHERES.
   if (sphNum >= RTG_MAX_SPHERES) {
@@ -599,6 +644,7 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
   ctx->hasScene = true;
+  ++ctx->sceneGen;  // new geometry keys: no launch-order feedback from the old scene
   const auto tEnd = clk::now();
   ctx->sceneStats[0] = std::chrono::duration<double, std::milli>(tUp - tPack).count();
   ctx->sceneStats[1] = std::chrono::duration<double, std::milli>(tEnd - tUp).count();
@@ -611,6 +657,33 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
                                     sizeof(unsigned));
   ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / kBvhWords);
   return RTG_OK;
+}
+
+// The launch-order feedback's key of a frame geometry: everything that
+// decides which pixel group an index names and what it costs (FNV-1a; a
+// collision only mis-orders a launch, the frame is the same).
+static unsigned long long geometry_key(unsigned width, unsigned height, float zoom,
+                                       float aliasFactor, int stackSize, unsigned rowBlock,
+                                       unsigned shard, unsigned nShards, const unsigned* rowList,
+                                       unsigned nRowList, int variant, unsigned sceneGen) {
+  unsigned long long h = 1469598103934665603ull;
+  auto mix = [&h](unsigned long long v) {
+    for (int k = 0; k < 8; ++k) {
+      h ^= (v >> (8 * k)) & 0xFFu;
+      h *= 1099511628211ull;
+    }
+  };
+  unsigned zb, ab;
+  memcpy(&zb, &zoom, 4);
+  memcpy(&ab, &aliasFactor, 4);
+  mix(((unsigned long long)width << 32) | height);
+  mix(((unsigned long long)zb << 32) | ab);
+  mix(((unsigned long long)(unsigned)stackSize << 32) | rowBlock);
+  mix(((unsigned long long)shard << 32) | nShards);
+  mix((unsigned long long)(uintptr_t)rowList);
+  mix(((unsigned long long)nRowList << 32) | (unsigned)variant);
+  mix(sceneGen);
+  return h;
 }
 
 static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float zoom,
@@ -701,6 +774,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.groupCap = 0;
   a.lptMin = (unsigned)ctx->lptMin;
   a.nPersist = 0;
+  a.groupCost = nullptr;
+  a.costStat = nullptr;
+  a.costPrev = nullptr;
   if (variant == 120) {  // executed-work counting build
     if (!ctx->counts) {
       HIP_TRY(hipMalloc(&ctx->counts, 2 * kCntSlots * sizeof(unsigned long long)));
@@ -751,11 +827,44 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         slot->list = nullptr;
         slot->sel = nullptr;
         slot->cap = 0;
-        HIP_TRY(hipMalloc(&slot->list, groups * sizeof(unsigned)));
-        HIP_TRY(hipMalloc(&slot->sel, groups * sizeof(unsigned long long)));
+        // two halves of `groups` entries (the four runs, KernelArgs::groupCount)
+        HIP_TRY(hipMalloc(&slot->list, 2 * groups * sizeof(unsigned)));
+        HIP_TRY(hipMalloc(&slot->sel, 2 * groups * sizeof(unsigned long long)));
         slot->cap = groups;
       }
-      if (!slot->count) HIP_TRY(hipMalloc(&slot->count, 2 * sizeof(unsigned)));
+      if (!slot->count) HIP_TRY(hipMalloc(&slot->count, 4 * sizeof(unsigned)));
+      if (ctx->orderFeedback && !(ctx->opts.flags & RTG_LAUNCH_NO_ORDER_FEEDBACK)) {
+        // launch-order feedback: this frame geometry's entry (LRU)
+        const unsigned long long key = geometry_key(width, height, zoom, aliasFactor, stackSize,
+                                                    rowBlock, shard, nShards, rowList, nRowList,
+                                                    variant, ctx->sceneGen);
+        rtg_context::CostEntry* ce = nullptr;
+        for (auto& e : ctx->costs)
+          if (e.launches && e.key == key) ce = &e;
+        if (!ce) {
+          ce = &ctx->costs[0];
+          for (auto& e : ctx->costs)
+            if (e.lastUse < ce->lastUse) ce = &e;
+          if (ce->cap < groups) {
+            // an evicted entry's buffers may still be read by queued launches
+            HIP_TRY(hipDeviceSynchronize());
+            (void)hipFree(ce->cost);
+            ce->cost = nullptr;
+            ce->cap = 0;
+            HIP_TRY(hipMalloc(&ce->cost, groups * sizeof(unsigned)));
+            ce->cap = groups;
+          }
+          if (!ce->stat) HIP_TRY(hipMalloc(&ce->stat, 2 * sizeof(unsigned long long)));
+          ce->key = key;
+          ce->launches = 0;
+        }
+        ce->lastUse = ++ctx->costClock;
+        a.groupCost = ce->cost;
+        a.costStat = ce->stat + ce->cur;
+        a.costPrev = ce->launches ? ce->stat + (1 - ce->cur) : nullptr;
+        ce->cur = 1 - ce->cur;
+        ++ce->launches;
+      }
       cullGroups = groups;  // the cull pass is enqueued below, after the last failure point
       // about one wave per listed group: the benchmark scenes list 13-17 % of
       // their groups; a wave past the count exits at once, and a scene that
@@ -804,7 +913,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // so an error never leaves a cull pass (which zero-fills dst and fills the
   // slot's list) in flight without the slot's event behind it.
   if (slot) {
-    HIP_TRY(hipMemsetAsync(slot->count, 0, 2 * sizeof(unsigned), (hipStream_t)stream));
+    HIP_TRY(hipMemsetAsync(slot->count, 0, 4 * sizeof(unsigned), (hipStream_t)stream));
+    if (a.costStat)
+      HIP_TRY(hipMemsetAsync(a.costStat, 0, sizeof(unsigned long long), (hipStream_t)stream));
     hipLaunchKernelGGL(
         cull_groups_kernel,
         dim3((unsigned)((cullGroups + 256 * kCullRounds - 1) / (256 * kCullRounds))), dim3(256),

@@ -304,6 +304,11 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
       if (overlap_keep(spheres, h, j)) rec(ps->ovRec, j);
     ps->ovOff.push_back((unsigned)(ps->ovRec.size() / kListWords));
   }
+  // one padding record past each table's end: the kernel reads records in
+  // pairs (one 64-byte scalar load) and ignores the second past a list's end
+  const float pad[kListWords] = {NAN, NAN, NAN, NAN, NAN, NAN, 0.f, 1.f};
+  ps->capRec.insert(ps->capRec.end(), pad, pad + kListWords);
+  ps->ovRec.insert(ps->ovRec.end(), pad, pad + kListWords);
 }
 
 // Secondary-ray cone masks.  A secondary ray of sphere h starts in the origin

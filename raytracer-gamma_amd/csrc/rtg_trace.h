@@ -249,8 +249,9 @@ enum : int { kProbeSplitBase = 100, kProbeSplitSetup = 101, kProbeSplitContain =
 // the pre-computed reflection ray is only read when that child is traced.
 struct FrameC {
   float cx, cy, cz;
-  unsigned meta;  // rm << 9 | (1 + origin sphere) << 2 | flags (bit0: stage 2,
-                  // bit1: reflection child significant)
+  unsigned meta;  // rm << 10 | inside << 9 | (1 + origin sphere) << 2 | flags
+                  // (bit0: stage 2, bit1: reflection child significant;
+                  // inside: the reflection child starts inside the origin sphere)
 };
 struct FrameR { V3 ro, rd, rI; };
 
@@ -909,9 +910,15 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           FrameC f;
           f.cx = colour.x; f.cy = colour.y; f.cz = colour.z;
           // bits 2..8: 1 + the sphere whose origin ball holds the
-          // reflection ray's origin P + 0.01 rd (cone cull, n <= 64), or 0
-          f.meta = ((unsigned)rm << 9) |
-                   ((unsigned)(sc.has_cone() && guardOK ? hit + 1 : 0) << 2) | (sigR ? 2u : 0u);
+          // reflection ray's origin P + 0.01 rd (cone cull, n <= 64), or 0;
+          // bit 9: the hit came from inside that sphere (d.N > 0), so its
+          // reflection turns back into it: the child is traced like an
+          // entering ray (closest_enter, which checks that it stays in the
+          // sphere's guard ball and else takes the general query)
+          const bool origin = sc.has_cone() && guardOK;
+          const bool inside = Q == 4 && origin && vdot(d, N) > 0.f;
+          f.meta = ((unsigned)rm << 10) | (inside ? 0x200u : 0u) |
+                   ((unsigned)(origin ? hit + 1 : 0) << 2) | (sigR ? 2u : 0u);
           fc.set(lv, f);
           if (sigR) {
             sc.count(kCntReflPush, 1);
@@ -983,8 +990,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
                        "v"(rx.rd.z), "v"(rx.rI.x), "v"(rx.rI.y), "v"(rx.rI.z));
         }
 #endif
-        o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 9);
+        o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 10);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
+        if (Q == 4 && (f.meta & 0x200u)) enterH = originH;  // reflection back into it
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
         descend = true;
         break;
@@ -1248,6 +1256,12 @@ RTG_HD float norm_up(float a) { return sqrt_hw(a) * (1.0f + 0x1p-20f); }
 //   ch[k]          > 0 child node, < 0 ~sphere index, 0 empty
 //   cr[k]          a sphere slot's containment radius^2 (r + 1e-6f)^2
 constexpr int kBvhWords = 32;
+// One record of a sphere list (sphere_lists, rtg_scene_pack.h).
+struct ListRec {
+  V3 c;
+  float rs, r2, cr, rf;
+  int idx;
+};
 struct BvhRec {
   float s[24];
   int ch[4];
@@ -1257,13 +1271,23 @@ struct BvhRec {
 // Children of a node in front-to-back order for the wave: of the valid
 // (child, key) pairs, keys = a lane's box entry parameter (wave-uniform), the
 // nearest is returned (the next node: no stack round trip) and the others are
-// pushed farthest first.  Five compare-exchanges.
-RTG_HD int push_sorted(BvhStack& st, int c0, float k0, int c1, float k1, int c2, float k2,
-                       int c3, float k3) {
-  auto cx = [](int& ca, float& ka, int& cb, float& kb) {
+// pushed farthest first.  Five compare-exchanges.  The keys are compared as
+// unsigned bit patterns: an entry parameter is max(..., 0) >= 0 and never NaN
+// (slab_pass), and for such floats the patterns order like the values (a -0
+// would sort last; the order only decides which node is visited first, never
+// an answer), so the compare-exchanges are scalar integer work.
+RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2, float f2,
+                       int c3, float f3) {
+  auto bits = [](float f) {
+    unsigned u;
+    memcpy(&u, &f, 4);
+    return u;
+  };
+  unsigned k0 = bits(f0), k1 = bits(f1), k2 = bits(f2), k3 = bits(f3);
+  auto cx = [](int& ca, unsigned& ka, int& cb, unsigned& kb) {
     if (kb > ka) {
       const int ct = ca; ca = cb; cb = ct;
-      const float kt = ka; ka = kb; kb = kt;
+      const unsigned kt = ka; ka = kb; kb = kt;
     }
   };
   cx(c0, k0, c1, k1);
@@ -1296,7 +1320,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
                         bool shadowQ = false) {
   BvhRec r;
-  sc.bvh_rec(nd, r);
+  sc.bvh_rec_ray(nd, r);
   int pc[4];
   float pk[4];
 #pragma unroll
@@ -1452,6 +1476,9 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
 // and the list is ordered nearest first, so blocked lanes stop early; the
 // wave leaves once every lane is blocked.  Same answer as blocked_bvh: any
 // blocker.
+// The list loops below take records in pairs, k and k + 1, from one 64-byte
+// scalar load (cap_rec2 / ov_rec2), so a wave waits on half as many loads;
+// the second record of a pair past the list's end is not used.
 template <class Scene>
 RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h) {
   sc.count(kUQuery, 1);
@@ -1459,20 +1486,24 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
   unsigned k0, k1;
   sc.cap_range(l, (unsigned)h, k0, k1);
   bool blk = false;
-  for (unsigned k = k0; k < k1; ++k) {  // wave-uniform
+  auto step = [&](const ListRec& r) {
     sc.count(kUCapIter, 1);
-    float rs, r2, cr, rf;
-    int idx;
-    const V3 c = sc.cap_rec(k, rs, r2, cr, idx, rf);
-    if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
+    if (!blk && !(pass1_rad(q, r.c, r.rs) < 0.f)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere(q, c, r2, res);
+      const float t = ray_sphere(q, r.c, r.r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
       }
     }
+  };
+  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
+    ListRec r0, r1;
+    sc.cap_rec2(k, r0, r1);
+    step(r0);
+    if (sc.all(blk) || k + 1 >= k1) break;
+    step(r1);
     if (sc.all(blk)) break;
   }
   return blk;
@@ -1499,18 +1530,22 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
   int best = h;
   unsigned k0, k1;
   sc.ov_range((unsigned)h, k0, k1);
-  for (unsigned k = k0; k < k1; ++k) {  // wave-uniform
-    float rs, r2, cr, rf;
-    int j;
-    const V3 c = sc.ov_rec(k, rs, r2, cr, j, rf);
-    if (j == h) continue;
+  auto step = [&](const ListRec& r) {
+    const int j = r.idx;
+    if (j == h) return;
     sc.count(kUOvIter, 1);
-    if (!(pass1_rad(q, c, rs) < 0.f)) {
+    if (!(pass1_rad(q, r.c, r.rs) < 0.f)) {
       sc.count(kUEnterExact, 1);
       bool rj;
-      const float t = ray_sphere(q, c, r2, rj);
+      const float t = ray_sphere(q, r.c, r.r2, rj);
       if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
     }
+  };
+  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
+    ListRec r0, r1;
+    sc.ov_rec2(k, r0, r1);
+    step(r0);
+    if (k + 1 < k1) step(r1);
   }
   tOut = minT;
   return best;
@@ -1526,16 +1561,20 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
   nT = sc.refr((int)sc.n);  // background material
   unsigned k0, k1;
   sc.ov_range((unsigned)h, k0, k1);
-  for (unsigned k = k0; k < k1; ++k) {  // wave-uniform
+  auto step = [&](const ListRec& r) {
     sc.count(kUOvIter, 1);
-    float rs, r2, cr, rf;
-    int j;
-    const V3 c = sc.ov_rec(k, rs, r2, cr, j, rf);
-    const V3 dist = vsub(pt, c);
-    if (found < 0 && vdot(dist, dist) <= cr) {
-      found = j;
-      nT = rf;
+    const V3 dist = vsub(pt, r.c);
+    if (found < 0 && vdot(dist, dist) <= r.cr) {
+      found = r.idx;
+      nT = r.rf;
     }
+  };
+  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
+    ListRec r0, r1;
+    sc.ov_rec2(k, r0, r1);
+    step(r0);
+    if (sc.all(found >= 0) || k + 1 >= k1) break;
+    step(r1);
     if (sc.all(found >= 0)) break;
   }
   return found;

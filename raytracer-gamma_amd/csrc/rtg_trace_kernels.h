@@ -264,6 +264,31 @@ struct DevScene {
     rf = g[7];
     return v3(g[0], g[1], g[2]);
   }
+  // Records k and k + 1 of a list table with one 64-byte scalar load (the
+  // tables end with a padding record, sphere_lists).
+  __device__ __forceinline__ static void list_rec2(cfloat_p base, unsigned k, ListRec& r0,
+                                                   ListRec& r1) {
+    typedef float f16 __attribute__((ext_vector_type(16)));
+    const f16 g = *(const RTG_CONST f16*)fidx(base, 8u * k);
+    r0.c = v3(g[0], g[1], g[2]);
+    r0.rs = g[3];
+    r0.r2 = g[4];
+    r0.cr = g[5];
+    r0.idx = __float_as_int(g[6]);
+    r0.rf = g[7];
+    r1.c = v3(g[8], g[9], g[10]);
+    r1.rs = g[11];
+    r1.r2 = g[12];
+    r1.cr = g[13];
+    r1.idx = __float_as_int(g[14]);
+    r1.rf = g[15];
+  }
+  __device__ __forceinline__ void cap_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
+    list_rec2(capRec, k, r0, r1);
+  }
+  __device__ __forceinline__ void ov_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
+    list_rec2(ovRec, k, r0, r1);
+  }
   __device__ __forceinline__ V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
                                         float& rf) const {
     return list_rec(capRec, k, rs, r2, cr, idx, rf);
@@ -285,6 +310,29 @@ struct DevScene {
     for (int k = 0; k < 4; ++k) {
       r.ch[k] = __float_as_int(b[8 + k]);
       r.cr[k] = b[12 + k];
+    }
+  }
+  // The 28 words a ray query uses (the slots and child indices, not the
+  // containment radii): 64 + 32 + 16 bytes of scalar loads.  (Loading all 32
+  // words let the register allocator put the second 64-byte load over the
+  // first one's unused radii, and the overlapping destinations made it wait
+  // for the first load before issuing the second: two round trips per node.)
+  __device__ __forceinline__ void bvh_rec_ray(unsigned nd, BvhRec& r) const {
+    typedef float f16 __attribute__((ext_vector_type(16)));
+    typedef float f8 __attribute__((ext_vector_type(8)));
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    const RTG_CONST float* p = fidx(bvhNodes, kBvhWords * nd);
+    const f16 a = *(const RTG_CONST f16*)p;
+    const f8 b = *(const RTG_CONST f8*)(p + 16);
+    const i4 c = *(const RTG_CONST i4*)(p + 24);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r.s[k] = a[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.s[16 + k] = b[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r.ch[k] = c[k];
+      r.cr[k] = 0.f;  // not loaded
     }
   }
   // One lane's value for wave-uniform decisions (traversal order, cone cull).
@@ -482,10 +530,22 @@ struct KernelArgs {
   // may hit, their count, and the number of persistent waves; null otherwise.
   const unsigned* groupList;
   const unsigned long long* groupSel;  // the listed groups' primary-ray sphere masks
-  const unsigned* groupCount;  // [0] heavy groups (listed from the front), [1] light (from the back)
-  unsigned groupCap;           // the list's length (light entries end at groupCap - 1)
-  unsigned lptMin;             // cull_groups_kernel's heavy threshold
+  // The list holds 2 x groupCap entries in four runs, read in this order:
+  // [0, count[0]) from the front of the first half, count[1] entries from its
+  // back (groupCap - 1 down), count[2] from the front of the second half and
+  // count[3] from its back (2 groupCap - 1 down); heaviest run first
+  // (cull_groups_kernel).
+  const unsigned* groupCount;  // [4] the runs' lengths
+  unsigned groupCap;
+  unsigned lptMin;             // cull_groups_kernel's popcount threshold (no cost feedback)
   unsigned nPersist;
+  // Launch-order feedback (compacted launches; null when off): each listed
+  // group's trace time in 10 ns ticks (s_memrealtime), written by this launch
+  // and read by the next launch of the same frame geometry, and the launches'
+  // sums: low 40 bits the ticks, high 24 bits the group count.
+  unsigned* groupCost;
+  unsigned long long* costStat;        // this launch's sums (zeroed before the cull pass)
+  const unsigned long long* costPrev;  // the previous launch's, or null
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
   unsigned long long* counts;  // 2 x kCntSlots unit counters (counting build, variant 120)
   uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
@@ -674,6 +734,22 @@ __device__ __forceinline__ void record_wave(const KernelArgs& a, unsigned t0, si
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
   const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
   if ((threadIdx.x & 63u) == 0) a.timeline[w] = make_uint4(t0, t1, hw, xcc | (tag << 4));
+}
+// The same record in two halves: the start at once (so the start time need
+// not stay live through the wave), the rest at the end.
+__device__ __forceinline__ void record_wave_start(const KernelArgs& a, unsigned t0, size_t w) {
+  if (a.timeline != nullptr && (threadIdx.x & 63u) == 0) a.timeline[w].x = t0;
+}
+__device__ __forceinline__ void record_wave_end(const KernelArgs& a, size_t w, unsigned tag) {
+  if (a.timeline == nullptr) return;
+  const unsigned t1 = (unsigned)__builtin_amdgcn_s_memrealtime();
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
+  if ((threadIdx.x & 63u) == 0) {
+    a.timeline[w].y = t1;
+    a.timeline[w].z = hw;
+    a.timeline[w].w = xcc | (tag << 4);
+  }
 }
 
 // Tile kernels: one 8 x 8 pixel tile per wave, all samples of a pixel in its
@@ -916,18 +992,40 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
     const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
     // variant 24: the wave recomputes its primary cull (no cull-pass masks)
     const RTG_CONST unsigned long long* gsel = (const RTG_CONST unsigned long long*)a.groupSel;
-    const unsigned nHeavy = ((const RTG_CONST unsigned*)a.groupCount)[0];
-    const unsigned cnt = nHeavy + ((const RTG_CONST unsigned*)a.groupCount)[1];
-    for (unsigned idx = (unsigned)gw; idx < cnt; idx += a.nPersist) {
-      // heavy run from the front, then the light run from the back
-      const unsigned at = idx < nHeavy ? idx : a.groupCap - 1u - (idx - nHeavy);
+    // List position of run-order index idx (the four runs, heaviest first),
+    // or ~0u past the end; the run lengths are read afresh (scalar loads)
+    // rather than held in SGPRs through the trace.
+    auto pos = [](unsigned idx) {
+      const RTG_CONST KernelArgs* b = kargs();
+      const RTG_CONST unsigned* gc = (const RTG_CONST unsigned*)b->groupCount;
+      const unsigned cap = b->groupCap;
+      const unsigned e0 = gc[0], e1 = e0 + gc[1], e2 = e1 + gc[2], e3 = e2 + gc[3];
+      return idx < e0 ? idx
+           : idx < e1 ? cap - 1u - (idx - e0)
+           : idx < e2 ? cap + (idx - e1)
+           : idx < e3 ? 2u * cap - 1u - (idx - e2)
+                      : ~0u;
+    };
+    record_wave_start(a, t0, gw);
+    unsigned tg = t0;  // this group's start (the first one's includes the wave's set-up)
+    for (unsigned idx = (unsigned)gw;; idx += kargs()->nPersist) {
+      const unsigned at = pos(idx);
+      if (at == ~0u) break;
       const unsigned g = __builtin_amdgcn_readfirstlane(list[at]);
       trace_group<S, Q, kDiag, decltype(sc), (kVariant == 19), (kVariant == 50)>(
           a, sc, g, kVariant != 24, kVariant != 24 ? (uint64_t)gsel[at] : 0ull);
+      const unsigned now = (unsigned)__builtin_amdgcn_s_memrealtime();
+      const RTG_CONST KernelArgs* b = kargs();
+      if (b->groupCost != nullptr && (threadIdx.x & 63u) == 0) {
+        // launch-order feedback for the next launch (vector stores and atomic)
+        b->groupCost[g] = now - tg;
+        atomicAdd(b->costStat, (1ull << 40) | (unsigned long long)(now - tg));
+      }
+      tg = now;
     }
-    if (a.timeline != nullptr && gw < cnt) {  // timeline tag: the wave's first group
-      const unsigned at = (unsigned)gw < nHeavy ? (unsigned)gw
-                                                : a.groupCap - 1u - ((unsigned)gw - nHeavy);
+    const unsigned at0 = a.timeline != nullptr ? pos((unsigned)gw) : ~0u;
+    if (at0 != ~0u) {  // timeline tag: the wave's first group
+      const unsigned at = at0;
       const unsigned g = list[at];
       tag = ((unsigned)__builtin_popcountll(gsel[at]) & 127u) | ((g < 0x1FFFFFu ? g : 0x1FFFFFu) << 7);
     }
@@ -938,7 +1036,8 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
                                                                                  gw * K + k);
   }
   if constexpr (kCount) sc.flush_counts(kargs()->counts);
-  record_wave(a, t0, gw, tag);
+  if constexpr (kList) record_wave_end(a, gw, tag);
+  else record_wave(a, t0, gw);
 }
 
 template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,

@@ -380,6 +380,7 @@ class Context:
                 "bvh_nodes": int(out[3])}
 
     LAUNCH_TIMELINE = 1  # RTG_LAUNCH_TIMELINE
+    LAUNCH_NO_ORDER_FEEDBACK = 2  # RTG_LAUNCH_NO_ORDER_FEEDBACK
     SEMANTICS_CPU, SEMANTICS_OPENCL = 0, 1  # RTG_SEMANTICS_*
 
     def set_semantics(self, semantics: int):

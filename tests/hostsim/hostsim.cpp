@@ -54,6 +54,16 @@ struct HostScene {
     rf = g[7];
     return rtg::v3(g[0], g[1], g[2]);
   }
+  static void list_rec2(const float* b, unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) {
+    r0.c = list_rec(b, k, r0.rs, r0.r2, r0.cr, r0.idx, r0.rf);
+    r1.c = list_rec(b, k + 1, r1.rs, r1.r2, r1.cr, r1.idx, r1.rf);
+  }
+  void cap_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
+    list_rec2(capRec, k, r0, r1);
+  }
+  void ov_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
+    list_rec2(ovRec, k, r0, r1);
+  }
   rtg::V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
     return list_rec(capRec, k, rs, r2, cr, idx, rf);
   }
@@ -71,6 +81,7 @@ struct HostScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   int* bvh_stack() const { return nullptr; }
+  void bvh_rec_ray(unsigned nd, rtg::BvhRec& r) const { bvh_rec(nd, r); }
   void bvh_rec(unsigned nd, rtg::BvhRec& r) const {
     const float* g = bvhNodes + (size_t)rtg::kBvhWords * nd;
     memcpy(r.s, g, 24 * 4);

@@ -224,6 +224,62 @@ def test_sharded_render_assembles_to_full_frame(R, golden, torch_cuda):
     ctx.close()
 
 
+def test_launch_order_feedback_keeps_frames(R, golden, torch_cuda):
+    """Launch-order feedback (cull_groups_kernel: groups listed by the previous
+    launch's measured times) only reorders work: repeated renders of one
+    geometry, more geometries than the context keeps (least recently used
+    entries replaced), row-list renders, a scene change and the flag that
+    turns it off all give the golden frame."""
+    from rtg_amd import dist
+    torch = torch_cuda
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    W, H, S, B = c["W"], c["H"], c["stack_size"], 8
+    ctx = R.Context(0)
+    ctx.set_scene(sph, lg)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    for flags in (0, ctx.LAUNCH_NO_ORDER_FEEDBACK, 0):
+        ctx.set_variant(0, flags)
+        for _ in range(3):
+            out.fill_(5.0)
+            ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=stream)
+            torch.cuda.synchronize()
+            assert canon_md5(out.cpu().numpy()) == c["fb_md5"], flags
+    ctx.set_variant(0, 0)
+    G = 12  # 12 shard geometries > the 8 kept: two passes replace entries
+    Rmax = dist.padded_rows(H, B, G)
+    buf = torch.zeros((G, Rmax, W, 3), dtype=torch.float32, device="cuda")
+    for _ in range(2):
+        for g in range(G):
+            ctx.render_device(W, H, buf[g].data_ptr(), stack_size=S, row_block=B, shard=g,
+                              n_shards=G, stream=stream)
+        torch.cuda.synchronize()
+        assert canon_md5(dist.assemble(buf, H, B).cpu().numpy()) == c["fb_md5"]
+    rows = torch.arange(H - 1, -1, -1, dtype=torch.int32, device="cuda")  # bottom up
+    for _ in range(2):
+        out.fill_(5.0)
+        ctx.render_rows_device(W, H, rows.data_ptr(), H, out.data_ptr(), stack_size=S,
+                               stream=stream)
+        torch.cuda.synchronize()
+        assert canon_md5(out.flip(0).cpu().numpy()) == c["fb_md5"]
+    c3 = golden["configs"]["c1"]  # another scene, then back
+    sph3, lg3 = load_scene("c1", c3["spheres"], c3["lights"])
+    ctx.set_scene(sph3, lg3)
+    small = torch.empty((c3["H"], c3["W"], 3), dtype=torch.float32, device="cuda")
+    for _ in range(2):
+        ctx.render_device(c3["W"], c3["H"], small.data_ptr(), stack_size=c3["stack_size"],
+                          stream=stream)
+        torch.cuda.synchronize()
+        assert canon_md5(small.cpu().numpy()) == c3["fb_md5"]
+    ctx.set_scene(sph, lg)
+    for _ in range(2):
+        ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=stream)
+        torch.cuda.synchronize()
+        assert canon_md5(out.cpu().numpy()) == c["fb_md5"]
+    ctx.close()
+
+
 @pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23, 24])
 def test_variant_full_frames(R, golden, torch_cuda, variant):
     """Kernel mappings over whole frames, sharded frames, row lists and
@@ -299,11 +355,11 @@ def test_errors_are_returned_not_fatal(R):
         R.render(sph, lg, 8, 8, device=64)
     with pytest.raises(R.RtgError):
         R.render_rows(sph, lg, 8, 8, [8])
-    # scenes of RTG_MAX_SPHERES (2^23) spheres or more are rejected before the
-    # sphere array is read (the kernel's 23-bit index fields, 32-bit offsets)
+    # scenes of RTG_MAX_SPHERES (2^22) spheres or more are rejected before the
+    # sphere array is read (the kernel's 22-bit index fields, 32-bit offsets)
     ctx = R.Context(0)
     one = np.zeros(1, R.SPHERE_DTYPE)
-    rc = R.lib().rtg_context_set_scene(ctx._h, ctypes.c_void_p(one.ctypes.data), 1 << 23, None, 0)
+    rc = R.lib().rtg_context_set_scene(ctx._h, ctypes.c_void_p(one.ctypes.data), 1 << 22, None, 0)
     assert rc == -1 and b"spheres" in R.lib().rtg_last_error()
     ctx.close()
     # still usable afterwards
