@@ -161,11 +161,15 @@ constexpr unsigned kCullRounds = 4;
 // median), which dominates a short launch such as one GPU's shard of a
 // multi-GPU frame.  The groups are listed in four runs, heaviest first
 // (KernelArgs::groupCount):
-//  * with launch-order feedback (a.costPrev: the previous launch of the same
-//    frame geometry measured every listed group's trace time, and its mean
+//  * with launch-order feedback (a.groupCost: the previous launch of the same
+//    frame geometry wrote every listed group's trace time; a.costPrev: the
+//    sum and count of the times the previous cull pass read, whose mean is
 //    mu), by that time: >= 2 mu, >= mu, >= mu / 2, the rest.  A group's cost
 //    is a scheduling hint only: any value lists the group, so the frame is
-//    the same whatever the hint (a group dead last time reads a stale value);
+//    the same whatever the hint (a group dead last time reads a stale value).
+//    The pass also sums the times it reads into a.costStat, one atomic per
+//    block (the trace kernel's waves only store their group's time: 10^5
+//    atomics on one address from the trace waves cost a C3 frame 0.5 ms);
 //  * otherwise (first launch) by the sphere mask: >= a.lptMin spheres first.
 // Run 0 fills the list's first half from the front, run 1 from its back,
 // runs 2 and 3 the second half likewise.
@@ -175,6 +179,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
                                                           unsigned* groupCount) {
   __shared__ unsigned cnt[4][kCullRounds][4];
   __shared__ unsigned blockBase[4];
+  __shared__ unsigned long long waveCost[4];
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned PPW = 64u / (nAA * nAA);
@@ -188,6 +193,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     if (ng != 0u) mu = (float)(st & ((1ull << 40) - 1ull)) / (float)ng;
   }
   uint64_t live[4][kCullRounds], sel[kCullRounds];
+  unsigned long long costAcc = 0;  // this lane's listed groups: time sum (low 40), count
 #pragma unroll
   for (unsigned k = 0; k < kCullRounds; ++k) {
     const size_t g = blockG + k * 256 + threadIdx.x;
@@ -202,9 +208,14 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
       if (q1 > total * 3) q1 = total * 3;
       for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
     }
+    unsigned cost = 0;
+    if (a.costStat != nullptr && pc != 0u) {
+      cost = a.groupCost[g];
+      costAcc += (1ull << 40) | (unsigned long long)cost;
+    }
     unsigned run;
     if (mu > 0.f) {
-      const float c = (pc != 0u) ? (float)a.groupCost[g] : 0.f;
+      const float c = (float)cost;
       run = c >= 2.f * mu ? 0u : c >= mu ? 1u : c >= 0.5f * mu ? 2u : 3u;
     } else {
       run = pc >= a.lptMin ? 0u : 1u;
@@ -215,6 +226,11 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
       if (lane == 0) cnt[c][k][wave] = (unsigned)__builtin_popcountll(live[c][k]);
     }
   }
+  if (a.costStat != nullptr) {  // the wave's sum (butterfly), for this launch's stat
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) costAcc += __shfl_xor(costAcc, off, 64);
+    if (lane == 0) waveCost[wave] = costAcc;
+  }
   __syncthreads();
   if (threadIdx.x < 4) {
     const unsigned c = threadIdx.x;
@@ -222,6 +238,9 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     for (unsigned k = 0; k < kCullRounds; ++k)
       for (unsigned w = 0; w < 4; ++w) sum += cnt[c][k][w];
     blockBase[c] = sum ? atomicAdd(&groupCount[c], sum) : 0u;
+  } else if (threadIdx.x == 64 && a.costStat != nullptr) {
+    const unsigned long long t = waveCost[0] + waveCost[1] + waveCost[2] + waveCost[3];
+    if (t) atomicAdd(a.costStat, t);
   }
   __syncthreads();
   const unsigned cap = a.groupCap;
@@ -859,10 +878,13 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
           ce->launches = 0;
         }
         ce->lastUse = ++ctx->costClock;
+        // the trace kernel writes groupCost every launch; the cull pass reads
+        // it (and sums it into costStat) once a launch has written it, and
+        // orders by it once a cull pass has summed it (costPrev)
         a.groupCost = ce->cost;
-        a.costStat = ce->stat + ce->cur;
-        a.costPrev = ce->launches ? ce->stat + (1 - ce->cur) : nullptr;
-        ce->cur = 1 - ce->cur;
+        a.costStat = ce->launches >= 1 ? ce->stat + ce->cur : nullptr;
+        a.costPrev = ce->launches >= 2 ? ce->stat + (1 - ce->cur) : nullptr;
+        if (ce->launches >= 1) ce->cur = 1 - ce->cur;
         ++ce->launches;
       }
       cullGroups = groups;  // the cull pass is enqueued below, after the last failure point

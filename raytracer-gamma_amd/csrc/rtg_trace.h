@@ -1320,7 +1320,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
                         bool shadowQ = false) {
   BvhRec r;
-  sc.bvh_rec_ray(nd, r);
+  sc.bvh_rec(nd, r);
   int pc[4];
   float pk[4];
 #pragma unroll

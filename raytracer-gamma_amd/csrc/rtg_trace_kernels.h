@@ -312,29 +312,6 @@ struct DevScene {
       r.cr[k] = b[12 + k];
     }
   }
-  // The 28 words a ray query uses (the slots and child indices, not the
-  // containment radii): 64 + 32 + 16 bytes of scalar loads.  (Loading all 32
-  // words let the register allocator put the second 64-byte load over the
-  // first one's unused radii, and the overlapping destinations made it wait
-  // for the first load before issuing the second: two round trips per node.)
-  __device__ __forceinline__ void bvh_rec_ray(unsigned nd, BvhRec& r) const {
-    typedef float f16 __attribute__((ext_vector_type(16)));
-    typedef float f8 __attribute__((ext_vector_type(8)));
-    typedef int i4 __attribute__((ext_vector_type(4)));
-    const RTG_CONST float* p = fidx(bvhNodes, kBvhWords * nd);
-    const f16 a = *(const RTG_CONST f16*)p;
-    const f8 b = *(const RTG_CONST f8*)(p + 16);
-    const i4 c = *(const RTG_CONST i4*)(p + 24);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) r.s[k] = a[k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r.s[16 + k] = b[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      r.ch[k] = c[k];
-      r.cr[k] = 0.f;  // not loaded
-    }
-  }
   // One lane's value for wave-uniform decisions (traversal order, cone cull).
   __device__ __forceinline__ float first_lane(float v) const {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -540,12 +517,13 @@ struct KernelArgs {
   unsigned lptMin;             // cull_groups_kernel's popcount threshold (no cost feedback)
   unsigned nPersist;
   // Launch-order feedback (compacted launches; null when off): each listed
-  // group's trace time in 10 ns ticks (s_memrealtime), written by this launch
-  // and read by the next launch of the same frame geometry, and the launches'
-  // sums: low 40 bits the ticks, high 24 bits the group count.
+  // group's trace time in 10 ns ticks (s_memrealtime), written by the trace
+  // kernel and read by the next launch's cull pass of the same frame
+  // geometry, which also sums what it reads (low 40 bits the ticks, high 24
+  // the group count) for the launch after it.
   unsigned* groupCost;
-  unsigned long long* costStat;        // this launch's sums (zeroed before the cull pass)
-  const unsigned long long* costPrev;  // the previous launch's, or null
+  unsigned long long* costStat;        // this cull pass's sums (zeroed before it), or null
+  const unsigned long long* costPrev;  // the previous cull pass's, or null
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
   unsigned long long* counts;  // 2 x kCntSlots unit counters (counting build, variant 120)
   uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
@@ -1016,11 +994,8 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
           a, sc, g, kVariant != 24, kVariant != 24 ? (uint64_t)gsel[at] : 0ull);
       const unsigned now = (unsigned)__builtin_amdgcn_s_memrealtime();
       const RTG_CONST KernelArgs* b = kargs();
-      if (b->groupCost != nullptr && (threadIdx.x & 63u) == 0) {
-        // launch-order feedback for the next launch (vector stores and atomic)
-        b->groupCost[g] = now - tg;
-        atomicAdd(b->costStat, (1ull << 40) | (unsigned long long)(now - tg));
-      }
+      if (b->groupCost != nullptr && (threadIdx.x & 63u) == 0)
+        b->groupCost[g] = now - tg;  // launch-order feedback (a vector store)
       tg = now;
     }
     const unsigned at0 = a.timeline != nullptr ? pos((unsigned)gw) : ~0u;

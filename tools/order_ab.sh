@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # tools/order_ab.sh — GPU tests on the in-tree build, then the launch-order
 # A/B (tools/order_ab.py) interleaved over ROUNDS rounds: the previous
-# library (ab/librtg_base.so), the feedback build (ab/librtg_fb.so) with
+# library (ab/librtg_base.so), the feedback build (ab/librtg_fb2.so) with
 # feedback and with RTG_LAUNCH_ORDER=popcount, on C3 and C4.  Each GPU step
 # has its own time limit; the chain stops at the first failure.
 set -o pipefail
@@ -15,8 +15,8 @@ fi
 for r in $(seq ${ROUNDS:-3}); do
   for c in ${CONFIGS:-c3 c4}; do
     RTG_LIB=$PWD/ab/librtg_base.so timeout -k 10 300 python tools/order_ab.py --config $c | tee -a $OUT/ab.jsonl || exit 1
-    RTG_LIB=$PWD/ab/librtg_fb.so timeout -k 10 300 python tools/order_ab.py --config $c | tee -a $OUT/ab.jsonl || exit 1
-    RTG_LAUNCH_ORDER=popcount RTG_LIB=$PWD/ab/librtg_fb.so timeout -k 10 300 python tools/order_ab.py --config $c | tee -a $OUT/ab.jsonl || exit 1
+    RTG_LIB=$PWD/ab/librtg_fb2.so timeout -k 10 300 python tools/order_ab.py --config $c | tee -a $OUT/ab.jsonl || exit 1
+    RTG_LAUNCH_ORDER=popcount RTG_LIB=$PWD/ab/librtg_fb2.so timeout -k 10 300 python tools/order_ab.py --config $c | tee -a $OUT/ab.jsonl || exit 1
   done
 done
 echo "== done"
