@@ -222,8 +222,11 @@ def main():
     grow = torch.tensor(R.shard_row_indices(H, B, rank, world).astype(np.int64),
                         dtype=torch.int32, device="cuda") if world > 1 else None
     # chunks render on two streams in turn, so one chunk's last waves overlap
-    # the next chunk's first ones (a launch ends with a tail of long waves)
+    # the next chunk's first ones (a launch ends with a tail of long waves);
+    # rank 0 restores each chunk's row order on a third stream as soon as that
+    # chunk has arrived, overlapping the later chunks' rendering
     rstreams = [torch.cuda.Stream(), torch.cuda.Stream()] if world > 1 else None
+    astream = torch.cuda.Stream() if (world > 1 and rank == 0) else None
 
     frame = None
 
@@ -243,6 +246,8 @@ def main():
             ev_k[i][0].record(stream)
         for rs in rstreams:
             rs.wait_stream(stream)
+        if astream is not None:
+            astream.wait_stream(stream)
         works = []
         for c in range(K):
             r0, r1 = bounds[c], bounds[c + 1]
@@ -265,24 +270,31 @@ def main():
                         for g in range(world):
                             gathered[c][g].copy_(gl[g])
                     works.append(None)
+            if astream is not None:  # rank 0: chunk c in row order once it has arrived
+                with torch.cuda.stream(astream):
+                    if works[c] is not None:
+                        works[c].wait()  # astream waits for chunk c's gather
+                    else:
+                        astream.wait_stream(rs)  # the host-memory copies above
+                    if i is not None and c == K - 1:
+                        ev_g[i].record(astream)
+                    hc = min(H - r0 * world, (r1 - r0) * world)
+                    if hc > 0:  # native permute kernel, at global row r0 G
+                        ctx.assemble_shards_device(gathered[c].data_ptr(), world, r1 - r0, W, hc,
+                                                   B, frame_buf.data_ptr() + 12 * W * r0 * world,
+                                                   stream=astream.cuda_stream)
         for rs in rstreams:
             stream.wait_stream(rs)
         if i is not None:
             ev_k[i][1].record(stream)
-        for c in range(K):
-            if works[c] is not None:
-                works[c].wait()  # the current stream waits for chunk c's gather
-            if i is not None and c == K - 1:
-                ev_g[i].record(stream)
-            if rank == 0:  # chunk c in row order (native permute kernel), at global row r0 G
-                r0, r1 = bounds[c], bounds[c + 1]
-                hc = min(H - r0 * world, (r1 - r0) * world)
-                if hc > 0:
-                    ctx.assemble_shards_device(gathered[c].data_ptr(), world, r1 - r0, W, hc, B,
-                                               frame_buf.data_ptr() + 12 * W * r0 * world,
-                                               stream=sptr)
-        if i is not None:
-            ev_a[i].record(stream)
+        if astream is not None:
+            if i is not None:
+                ev_a[i].record(astream)
+            stream.wait_stream(astream)
+        else:
+            for w in works:  # the shard is rendered into again next step
+                if w is not None:
+                    w.wait()
         if rank == 0:
             frame = frame_buf
 
@@ -317,8 +329,12 @@ def main():
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [round(float(x[0]), 4) for x in allr]
-        gather_tail = float(np.mean([ev_k[i][1].elapsed_time(ev_g[i]) for i in range(args.steps)]))
-        assemble = float(np.mean([ev_g[i].elapsed_time(ev_a[i]) for i in range(args.steps)]))
+        if rank == 0:  # its events (the assembling stream's)
+            gather_tail = float(np.mean([ev_k[i][1].elapsed_time(ev_g[i])
+                                         for i in range(args.steps)]))
+            assemble = float(np.mean([ev_g[i].elapsed_time(ev_a[i]) for i in range(args.steps)]))
+        else:
+            gather_tail = assemble = 0.0
         multi = {"render_ms_per_rank": per_rank,
                  "render_imbalance": round(max(per_rank) / (sum(per_rank) / world), 4),
                  "gather_tail_ms_rank0": round(gather_tail, 4),
@@ -328,8 +344,9 @@ def main():
                  "note": "render = this rank's shard chunks (HIP events, chunks on two "
                          "streams in turn); gather tail = end of rank 0's render to the last "
                          "gathered chunk on its stream (earlier chunks' gathers and assembles "
-                         "overlap rendering); assemble = the last chunk's row-order restore "
-                         "on rank 0; step = wall time per frame, max over ranks"}
+                         "overlap rendering); assemble = the last chunk's arrival to the end of "
+                         "its row-order restore on rank 0 (each chunk is restored on a third "
+                         "stream as it arrives); step = wall time per frame, max over ranks"}
     else:
         kern_max_ms = kern_ms
 

@@ -364,6 +364,17 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
         for (int k = 0; k < 3; ++k) cc[(size_t)cell * 3 + k] = c[k];
         cb[cell] = beta;
       }
+  // The angle test ang(cell centre, u) > X with X = A + beta_cell, A = alpha +
+  // tier + 1e-3, is taken as cos: for X < pi, acos(dt) > X  <=>  dt < cos X,
+  // and cos X = cos A cos beta - sin A sin beta from per-(h, i, tier) and
+  // per-cell values; a sphere is kept when dt >= cos X - 1e-12 (the margin
+  // covers the rounding of both sides, so the masks keep at least what the
+  // acos form kept), and always when X >= pi.
+  std::vector<double> cbc(kConeCells), cbs(kConeCells);
+  for (int cell = 0; cell < kConeCells; ++cell) {
+    cbc[cell] = cos(cb[cell]);
+    cbs[cell] = sin(cb[cell]);
+  }
   for (unsigned h = 0; h < n; ++h) {
     const rtg_sphere& sh = spheres[h];
     const double ch = fabs((double)sh.pos.x) + fabs((double)sh.pos.y) + fabs((double)sh.pos.z);
@@ -376,22 +387,24 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
       const double D = sqrt(ux * ux + uy * uy + uz * uz);
       const double ri = fabs((double)si.radius);
       const double rr = ri + 0x1p-8 * (D + rho + ri);
-      bool all = (i == h) || !(D > (rho + rr) * (1.0 + 1e-9));
+      const bool all = (i == h) || !(D > (rho + rr) * (1.0 + 1e-9));
       double alpha = 0.0;
       if (!all) alpha = asin(fmin(1.0, rr / (D - rho))) + asin(fmin(1.0, rho / D));
-      for (int tier = 0; tier < kConeTiers; ++tier)
+      for (int tier = 0; tier < kConeTiers; ++tier) {
+        const double A = alpha + kConeHalf[tier] + 1e-3;
+        const double cA = cos(A), sA = sin(A);
         for (int cell = 0; cell < kConeCells; ++cell) {
-          bool keep = all || alpha + kConeHalf[tier] + 1e-3 >= kPi;
+          bool keep = all || A + cb[cell] >= kPi;
           if (!keep) {
             const double* c = &cc[(size_t)cell * 3];
             const double dt = (c[0] * ux + c[1] * uy + c[2] * uz) / D;
-            const double ang = acos(fmin(1.0, fmax(-1.0, dt)));
-            keep = !(ang > alpha + kConeHalf[tier] + cb[cell] + 1e-3);
+            keep = dt >= cA * cbc[cell] - sA * cbs[cell] - 1e-12;
           }
           if (keep)
             (*out)[(((size_t)h * kConeTiers + tier) * kConeCells + cell) * 2 + (i >> 5)] |=
                 1u << (i & 31);
         }
+      }
     }
   }
 }

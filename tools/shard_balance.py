@@ -10,8 +10,10 @@ max/mean, and the predicted G-GPU frame time
     T_G = max_g t_g + gather tail + assemble
 with the gather tail = the last of K = 4 pipelined chunks of the largest
 shard over one xGMI link (the other chunks overlap rendering; 7 x 153 GB/s
-links per GPU, ~100 GB/s of it sustained per peer) and the assemble = one
-read + write of the frame on the root at ~5 TB/s.  speedup_G = T_1 / T_G.
+links per GPU, ~100 GB/s of it sustained per peer) and the assemble = the last
+chunk's read + write on the root at ~5 TB/s (bench.py restores each chunk's
+row order on a third stream as it arrives, so the earlier chunks' restores
+overlap rendering).  speedup_G = T_1 / T_G.
 
   python tools/shard_balance.py [--config c4] [--blocks 4,8,16] [--json OUT]
 """
@@ -85,7 +87,7 @@ def main():
     out = {"config": a.config, "W": W, "H": H, "frame_ms_1gpu": round(t1, 4),
            "frame_valu_slots": w1, "assumptions": {
                "gather_tail": f"last of {CHUNKS} chunks of the largest shard over one link at "
-                              f"{LINK_GBS} GB/s", "assemble": f"frame read+write at {ASSEMBLE_GBS} GB/s"},
+                              f"{LINK_GBS} GB/s", "assemble": f"the last of {CHUNKS} chunks' read+write at {ASSEMBLE_GBS} GB/s"},
            "cases": []}
     for B in [int(x) for x in a.blocks.split(",")]:
         for G in [int(x) for x in a.ranks.split(",")]:
@@ -97,7 +99,7 @@ def main():
             Rmax = rdist.padded_rows(H, B, G)
             shard_bytes = Rmax * W * 12
             gather_tail = (shard_bytes / CHUNKS) / (LINK_GBS * 1e9) * 1e3 if G > 1 else 0.0
-            assemble = (2 * W * H * 12) / (ASSEMBLE_GBS * 1e9) * 1e3 if G > 1 else 0.0
+            assemble = (2 * W * H * 12 / CHUNKS) / (ASSEMBLE_GBS * 1e9) * 1e3 if G > 1 else 0.0
             tG = max(ms) + gather_tail + assemble
             case = {"G": G, "B": B, "shard_ms": ms, "shard_valu_slots": wk,
                     "imbalance_time": round(max(ms) / (sum(ms) / G), 4),
