@@ -159,10 +159,14 @@ def main():
                     help="skip the counting-build run (executed-work roofline); PMC passes use "
                          "this so that only the timed kernel is profiled")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end frame timings")
-    ap.add_argument("--gather-chunks", type=int, default=4,
+    ap.add_argument("--gather-chunks", type=int, default=0,
                     help="N > 1: split each rank's rows into K chunks; each chunk is rendered "
                          "then gathered asynchronously, so RCCL overlaps the next chunk's "
-                         "rendering (1 = render all, then one gather)")
+                         "rendering (1 = render all, then one gather; 0 = by world size, "
+                         "rtg_amd.dist.default_chunks)")
+    ap.add_argument("--last-chunk-frac", type=float, default=-1.0,
+                    help="N > 1: the last chunk's share of the shard (0 = equal chunks; "
+                         "negative = by world size)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: gather through host memory (lets N ranks share one GPU "
                          "to exercise the multi-rank path on a 1-GPU box)")
@@ -214,8 +218,10 @@ def main():
     # the assemble kernel as soon as that chunk has arrived.  The global rows
     # of this rank's real rows, for rtg_render_rows_device.
     nblk = Rmax // B
-    K = max(1, min(args.gather_chunks, nblk)) if world > 1 else 1
-    bounds = [B * ((nblk * c) // K) for c in range(K + 1)]
+    auto_k, auto_f = rdist.default_chunks(world)
+    K = max(1, min(args.gather_chunks or auto_k, nblk)) if world > 1 else 1
+    last_frac = args.last_chunk_frac if args.last_chunk_frac >= 0.0 else auto_f
+    bounds = rdist.chunk_bounds(nblk, K, B, last_frac if world > 1 else 0.0)
     gathered = ([torch.empty((world, bounds[c + 1] - bounds[c], W, 3), dtype=torch.float32,
                              device="cuda") for c in range(K)]
                 if (world > 1 and rank == 0) else None)
@@ -341,6 +347,7 @@ def main():
                  "assemble_ms_rank0": round(assemble, 4),
                  "step_ms": round(elapsed / args.steps * 1e3, 4),
                  "gather_chunks": K,
+                 "chunk_rows": [bounds[c + 1] - bounds[c] for c in range(K)],
                  "note": "render = this rank's shard chunks (HIP events, chunks on two "
                          "streams in turn); gather tail = end of rank 0's render to the last "
                          "gathered chunk on its stream (earlier chunks' gathers and assembles "

@@ -31,3 +31,25 @@ def assemble(gathered, height: int, row_block: int):
     else:
         x = x.transpose(1, 0, 2, 3, 4)
     return x.reshape(nbmax * G * row_block, W, C)[:height]
+
+
+def chunk_bounds(n_blocks_shard: int, chunks: int, row_block: int, last_frac: float = 0.0):
+    """Row bounds of a shard split into `chunks` chunks of whole row blocks
+    (bench.py's pipelined gather): equal chunks (last_frac 0), or a last
+    chunk of about last_frac of the shard and the rest split equally, so the
+    gather left after the last render is short.  Every chunk holds >= 1 block."""
+    nb, K = n_blocks_shard, max(1, min(chunks, n_blocks_shard))
+    if last_frac <= 0.0 or K == 1:
+        return [row_block * ((nb * c) // K) for c in range(K + 1)]
+    lastb = max(1, min(nb - (K - 1), round(nb * last_frac)))
+    head = nb - lastb
+    return [row_block * ((head * c) // (K - 1)) for c in range(K)] + [row_block * nb]
+
+
+def default_chunks(world: int):
+    """(chunks, last_frac) of bench.py's N > 1 step, from the one-GPU
+    rehearsals of rank 0's part (tools/chunk_rehearsal.py,
+    profiles/r03/chunk_rehearsal.txt): every chunk is a launch that ends with
+    a tail of long waves, so an 8-way shard renders best in few chunks with a
+    short last one; 2- and 4-way shards in four equal chunks."""
+    return (3, 0.15) if world >= 8 else (4, 0.0)

@@ -80,3 +80,20 @@ def test_assemble_numpy_matches_torch(rtg):
     t = rdist.assemble(torch.from_numpy(g), H, B).numpy()
     assert (a == t).all()
     assert (a[:, 0, 0] == np.arange(H)).all()
+
+
+def test_chunk_bounds():
+    """bench.py's chunks of a shard: whole row blocks, in order, covering the
+    shard, each non-empty; with last_frac the last is about that share."""
+    from rtg_amd import dist
+    for nb in (1, 2, 3, 5, 34, 68, 135, 270):
+        for K in (1, 2, 3, 4, 8):
+            for f in (0.0, 0.15, 0.25, 0.5):
+                b = dist.chunk_bounds(nb, K, 8, f)
+                k = min(K, nb)
+                assert len(b) == k + 1 and b[0] == 0 and b[-1] == 8 * nb, (nb, K, f, b)
+                assert all(x % 8 == 0 for x in b)
+                assert all(b[i + 1] > b[i] for i in range(k)), (nb, K, f, b)
+                if f > 0 and k > 1 and nb >= 20:
+                    assert abs((b[-1] - b[-2]) / (8 * nb) - f) <= 1.0 / nb, (nb, K, f, b)
+    assert dist.default_chunks(8) == (3, 0.15) and dist.default_chunks(2) == (4, 0.0)
