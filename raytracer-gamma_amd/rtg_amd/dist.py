@@ -49,7 +49,8 @@ def chunk_bounds(n_blocks_shard: int, chunks: int, row_block: int, last_frac: fl
 def default_chunks(world: int):
     """(chunks, last_frac) of bench.py's N > 1 step, from the one-GPU
     rehearsals of rank 0's part (tools/chunk_rehearsal.py,
-    profiles/r03/chunk_rehearsal.txt): every chunk is a launch that ends with
-    a tail of long waves, so an 8-way shard renders best in few chunks with a
-    short last one; 2- and 4-way shards in four equal chunks."""
-    return (3, 0.15) if world >= 8 else (4, 0.0)
+    profiles/r03/chunks_c3_*.json, chunk_rehearsal.txt): every chunk is a
+    launch that ends with a tail of long waves, so a 4- or 8-way shard renders
+    best in three chunks and a 2-way one in four, the last one short (15 % of
+    the shard) so little of the gather is left after the last render."""
+    return (4, 0.15) if world <= 2 else (3, 0.15)

@@ -96,4 +96,4 @@ def test_chunk_bounds():
                 assert all(b[i + 1] > b[i] for i in range(k)), (nb, K, f, b)
                 if f > 0 and k > 1 and nb >= 20:
                     assert abs((b[-1] - b[-2]) / (8 * nb) - f) <= 1.0 / nb, (nb, K, f, b)
-    assert dist.default_chunks(8) == (3, 0.15) and dist.default_chunks(2) == (4, 0.0)
+    assert dist.default_chunks(8) == (3, 0.15) and dist.default_chunks(2) == (4, 0.15)

@@ -46,6 +46,9 @@ timeout -k 10 600 python tools/shard_balance.py --config c4 --blocks 8,16 --json
 timeout -k 10 600 python tools/shard_balance.py --config c3 --blocks 4,8 --json $OUT/shard_balance_c3.json > $OUT/shard_balance_c3.log 2>&1 &&
 tail -3 $OUT/shard_balance_c3.log &&
 echo "== profiles done" || exit 1
+echo "== chunk rehearsal (rank 0's part of the N > 1 step)" &&
+timeout -k 10 300 python tools/chunk_rehearsal.py --config c3 --ranks 2,4,8 --chunks 2,3,4 --last-frac 0.15 --json $OUT/chunks_c3_last15.json > /dev/null &&
+timeout -k 10 300 python tools/chunk_rehearsal.py --config c3 --ranks 2,4,8 --chunks 1,2,4 --json $OUT/chunks_c3_even.json > /dev/null &&
 echo "== 2-rank rehearsal (gloo gather, both ranks on this GPU)" &&
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
     bench.py --gpus 2 --steps 5 --warmup 1 --dist-backend gloo > $OUT/bench2_gloo.json 2> $OUT/bench2_gloo.err &&
