@@ -263,6 +263,18 @@ def test_launch_order_feedback_keeps_frames(R, golden, torch_cuda):
                                stream=stream)
         torch.cuda.synchronize()
         assert canon_md5(out.flip(0).cpu().numpy()) == c["fb_md5"]
+    # two streams rendering the same geometry at once share its cost table
+    # (a race on a scheduling hint only)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out2 = torch.empty_like(out)
+    for _ in range(3):
+        out.fill_(5.0)
+        out2.fill_(5.0)
+        ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=s1.cuda_stream)
+        ctx.render_device(W, H, out2.data_ptr(), stack_size=S, stream=s2.cuda_stream)
+        torch.cuda.synchronize()
+        assert canon_md5(out.cpu().numpy()) == c["fb_md5"]
+        assert canon_md5(out2.cpu().numpy()) == c["fb_md5"]
     c3 = golden["configs"]["c1"]  # another scene, then back
     sph3, lg3 = load_scene("c1", c3["spheres"], c3["lights"])
     ctx.set_scene(sph3, lg3)
