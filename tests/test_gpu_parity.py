@@ -270,6 +270,7 @@ def test_launch_order_feedback_keeps_frames(R, golden, torch_cuda):
     for _ in range(3):
         out.fill_(5.0)
         out2.fill_(5.0)
+        torch.cuda.synchronize()  # the fills (current stream) before s1 / s2 render
         ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=s1.cuda_stream)
         ctx.render_device(W, H, out2.data_ptr(), stack_size=S, stream=s2.cuda_stream)
         torch.cuda.synchronize()
