@@ -72,8 +72,10 @@ UNIT_COST = {
     # P (6), N = vnorm(P - c) (3 + 5 + 16 + 3), guard test (9), opacity terms and
     # colour (13)
     "U.shade": 55,
-    # L - P (3), gap (5), rcp_sqrt_rn (16), dir (3), incidence (5), test (1)
-    "U.light": 33,
+    # L - P (3), facing-away pre-test: N.dist (3), sum |N_k dist_k| (3), tests (3)
+    "U.light": 12,
+    # gap (5), rcp_sqrt_rn (16), dir (3), incidence (5), test (1)
+    "U.lightDir": 30,
     # mask-union predicates of the shadow ray
     "U.shadow": 3,
     # incidence / gap (10), sum += intensity * Lcol (6)
