@@ -149,7 +149,7 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
 }
 
 // A block takes kCullGroups = 4 x 256 consecutive groups (one per lane per
-// round) and appends its live ones with one atomic per class: the atomics on
+// round) and appends its live ones with one atomic per run: the atomics on
 // the counters serialise in L2, so one per wave cost ~70 us on C3.
 constexpr unsigned kCullRounds = 4;
 // Each listed group's sphere mask goes to groupSel at the same list index:
@@ -170,7 +170,8 @@ constexpr unsigned kCullRounds = 4;
 //    The pass also sums the times it reads into a.costStat, one atomic per
 //    block (the trace kernel's waves only store their group's time: 10^5
 //    atomics on one address from the trace waves cost a C3 frame 0.5 ms);
-//  * otherwise (first launch) by the sphere mask: >= a.lptMin spheres first.
+//  * otherwise (a geometry's first two launches, or feedback off) by the
+//    sphere mask: >= a.lptMin spheres first.
 // Run 0 fills the list's first half from the front, run 1 from its back,
 // runs 2 and 3 the second half likewise.
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
