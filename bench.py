@@ -138,6 +138,61 @@ def cpu_baseline(name, sph, lg, W, H, S, budget_s):
     return one, g1, o1
 
 
+def cpu_only(args):
+    """BASELINE configs[0] (C1: 640x480, 4 spheres, 1 light, depth 1): the
+    reference CPU path itself, no GPU.  The reference build (oracle/_ref,
+    raytracer.h compiled in place) renders the WHOLE frame with the
+    reference's loop (main.cpp:404-453) on one host thread and on all host
+    threads (<= 16); the frame and its PPM (savePPM, main.cpp:43-91) are
+    checked against the golden md5s.  One JSON line, n_gpus 0."""
+    W, H, n, m, depth = CONFIGS[args.config]
+    S = depth + 1
+    ref = os.path.join(ROOT, "oracle", "_ref", f"librtgref_S{S}.so")
+    if not os.path.exists(ref):
+        raise SystemExit(f"cpu-only: the reference build {ref} is missing (oracle/build_ref.sh)")
+    L = ctypes.CDLL(ref)
+    sph, lg = R.generate_scene(n, m, 42)
+    P = lambda a: ctypes.c_void_p(a.ctypes.data) if a.size else None  # noqa: E731
+    rows = np.arange(H, dtype=np.uint32)
+    golden = json.load(open(GOLDEN))["configs"].get(args.config, {})
+    legs = {}
+    for threads in sorted({1, cpu_threads()}):
+        times = []
+        for _ in range(max(1, args.steps)):
+            fb = np.zeros((H, W, 3), np.float32)
+            t0 = time.perf_counter()
+            L.ref_render_rows(P(sph), n, P(lg), m, W, H, ctypes.c_float(-4.0),
+                              ctypes.c_float(3.0), P(rows), H, P(fb), threads)
+            times.append(time.perf_counter() - t0)
+        med = float(np.median(times))
+        mx = R.max_colour_value(fb)
+        ppm = R.ppm_file_bytes(fb, mx)
+        legs[threads] = {"frame_ms": round(med * 1e3, 3), "value": round(W * H / med / 1e6, 3),
+                         "cores": threads, "runs": len(times),
+                         "fb_md5_match": canon_md5(fb) == golden.get("fb_md5"),
+                         "ppm_md5_match": hashlib.md5(ppm).hexdigest() == golden.get("ppm_md5")}
+    if args.ppm_out:
+        with open(args.ppm_out, "wb") as f:
+            f.write(ppm)
+    best = legs[max(legs)]
+    out = {"metric": METRIC, "value": best["value"], "unit": "Mpixels/s", "n_gpus": 0,
+           "steps": max(1, args.steps), "warmup": 0, "ms_per_step": best["frame_ms"],
+           "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic: seeded scene generator (SURVEY.md §8d, seed 42)",
+           "config": {"workload": f"{args.config}: {W}x{H}, {n} spheres, {m} lights, depth "
+                                  f"{depth}: the reference CPU path (raytracer.h), PPM out, no GPU",
+                      "width": W, "height": H, "spheres": n, "lights": m, "depth": depth},
+           "cpu_only": True,
+           "cpu_baseline": {"kind": "reference", "unit": "Mpixels/s", **best,
+                            "sample": f"{args.config}: the whole {W}x{H} frame, median of "
+                                      f"{best['runs']} runs",
+                            "single_thread": legs[1]},
+           "parity": {"fb_md5_match": best["fb_md5_match"] and legs[1]["fb_md5_match"],
+                      "ppm_md5_match": best["ppm_md5_match"] and legs[1]["ppm_md5_match"],
+                      "reference": "tests/golden (reference raytracer.h output)"}}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,7 +225,14 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: gather through host memory (lets N ranks share one GPU "
                          "to exercise the multi-rank path on a 1-GPU box)")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="BASELINE configs[0]: time the reference CPU path on the whole frame "
+                         "(no GPU), check its frame and PPM md5s; with --config c1")
+    ap.add_argument("--ppm-out", default="", help="--cpu-only: write the PPM here")
     args = ap.parse_args()
+    if args.cpu_only:
+        cpu_only(args)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -210,6 +272,9 @@ def main():
     ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for _ in range(args.steps)]
     # N > 1, rank 0: gather complete (after the waits) and assemble done
+    # N > 1, rank 0, all on the assembling stream (so their order is the
+    # stream's): every chunk rendered, the last chunk gathered, assembled
+    ev_r = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_g = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_a = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     # N > 1: chunks of the padded shard, whole row blocks (same row ranges on
@@ -278,6 +343,10 @@ def main():
                     works.append(None)
             if astream is not None:  # rank 0: chunk c in row order once it has arrived
                 with torch.cuda.stream(astream):
+                    if i is not None and c == K - 1:  # every chunk rendered (both streams)
+                        for rs_ in rstreams:
+                            astream.wait_stream(rs_)
+                        ev_r[i].record(astream)
                     if works[c] is not None:
                         works[c].wait()  # astream waits for chunk c's gather
                     else:
@@ -304,6 +373,17 @@ def main():
         if rank == 0:
             frame = frame_buf
 
+    # The first launch after set_scene (no launch-order feedback yet: the
+    # reference's single enqueue + clFinish, main.cpp:353-374), timed alone.
+    first_ms = None
+    if world == 1:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        first_ms = e0.elapsed_time(e1)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -335,8 +415,8 @@ def main():
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [round(float(x[0]), 4) for x in allr]
-        if rank == 0:  # its events (the assembling stream's)
-            gather_tail = float(np.mean([ev_k[i][1].elapsed_time(ev_g[i])
+        if rank == 0:  # its events, all on the assembling stream (non-negative)
+            gather_tail = float(np.mean([ev_r[i].elapsed_time(ev_g[i])
                                          for i in range(args.steps)]))
             assemble = float(np.mean([ev_g[i].elapsed_time(ev_a[i]) for i in range(args.steps)]))
         else:
@@ -349,8 +429,9 @@ def main():
                  "gather_chunks": K,
                  "chunk_rows": [bounds[c + 1] - bounds[c] for c in range(K)],
                  "note": "render = this rank's shard chunks (HIP events, chunks on two "
-                         "streams in turn); gather tail = end of rank 0's render to the last "
-                         "gathered chunk on its stream (earlier chunks' gathers and assembles "
+                         "streams in turn); gather tail = rank 0's last chunk rendered to the "
+                         "last chunk gathered, both events on its assembling stream (earlier "
+                         "chunks' gathers and assembles "
                          "overlap rendering); assemble = the last chunk's arrival to the end of "
                          "its row-order restore on rank 0 (each chunk is restored on a third "
                          "stream as it arrives); step = wall time per frame, max over ranks"}
@@ -470,15 +551,20 @@ def main():
         mxd = torch.empty(1, dtype=torch.float32, device="cuda")
         ppm_d = torch.empty(H * W * 3, dtype=torch.uint8, device="cuda")
         ppm_h = torch.empty(H * W * 3, dtype=torch.uint8, pin_memory=True)
-        t_full, t_d2h, t_ppm = [], [], []
+        t_full, t_d2h, t_ppm, t_cold = [], [], [], []
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(3):
             # scene upload (main.cpp:277-294) + render and finish (:353-374) +
-            # read-back of the float frame (:460)
+            # read-back of the float frame (:460); the render is the first
+            # after set_scene (no launch-order feedback)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             ctx.set_scene(sph, lg)
+            c0.record(stream)
             ctx.render_device(W, H, shard.data_ptr(), stack_size=S, row_block=B, stream=sptr)
+            c1.record(stream)
             torch.cuda.synchronize()
+            t_cold.append(c0.elapsed_time(c1))
             t1 = time.perf_counter()
             host.copy_(shard[:H], non_blocking=True)
             torch.cuda.synchronize()
@@ -501,10 +587,12 @@ def main():
                "scene_upload_ms": round(scene_stats["upload_ms"], 3),
                "scene_device_bytes": scene_stats["device_bytes"],
                "bvh_nodes": scene_stats["bvh_nodes"],
-               "render_ms": round(kern_ms, 4),
+               "render_ms": round(float(np.median(t_cold)), 4),
+               "render_fed_ms": round(kern_ms, 4),
                "d2h_fb_ms": round(float(np.median(t_d2h)), 3),
                "e2e_ppm_resident_scene_ms": round(float(np.median(t_ppm)), 3),
-               "note": "e2e_ms = set_scene (host masks/BVH + H2D) + render + D2H of the "
+               "note": "e2e_ms = set_scene (host masks/BVH + H2D) + render (the first after "
+                       "set_scene, no launch-order feedback: render_ms) + D2H of the "
                        f"{W * H * 12 / 1e6:.1f} MB float frame into pinned memory (main.cpp:277-"
                        "294, 353-374, 460); e2e_ppm_resident_scene_ms = render + device max + "
                        "PPM bytes + D2H of 3 B/px; medians of 3"}
@@ -581,6 +669,11 @@ def main():
                         else " + gloo gather") if world > 1 else "")},
         "mrays_per_s": round(mpx * 9, 1),
         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
+        "first_launch_ms": round(first_ms, 4) if first_ms is not None else None,
+        "timed_launches": {"first": 1 + args.warmup if world == 1 else None,
+                           "count": args.steps,
+                           "note": "trace-kernel dispatches [first, first + count) of this "
+                                   "process are the timed region's (tools/timed_stats.py)"},
         "roofline": roof, "cpu_baseline": cpu, "e2e": e2e, "multi_gpu": multi,
         "gpu_vs_cpu": round(mpx / cpu["value"], 1) if cpu else None,
         "parity": parity,

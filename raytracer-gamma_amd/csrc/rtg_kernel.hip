@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
       for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
     }
     unsigned cost = 0;
-    if (a.costStat != nullptr && pc != 0u) {
+    if (a.costStat != nullptr && a.groupCost != nullptr && pc != 0u) {
       cost = a.groupCost[g];
       costAcc += (1ull << 40) | (unsigned long long)cost;
     }
@@ -301,10 +301,16 @@ struct rtg_context {
   // Compacted-launch scratch: a ring of slots, so that renders of one
   // context on different streams can overlap; a slot is reused only after
   // the event recorded behind its last trace kernel.
+  // Its buffers are stream-ordered allocations (hipMallocAsync / hipFreeAsync
+  // behind the slot's event), so growing them never blocks the host or other
+  // streams.  count holds two sets of the four run lengths, used by
+  // alternate launches: each launch's trace kernel zeroes the other set for
+  // the next one (KernelArgs::zeroCount), so no memset precedes a cull pass.
   struct GroupSlot {
     unsigned* list = nullptr;  // listed pixel groups
     unsigned long long* sel = nullptr;  // their primary-ray sphere masks
-    unsigned* count = nullptr;
+    unsigned* count = nullptr;  // [2][4]
+    unsigned parity = 0;
     size_t cap = 0;
     hipEvent_t done = nullptr;
   };
@@ -315,6 +321,9 @@ struct rtg_context {
   // groups' measured trace times of its last launch and the last two
   // launches' sums; a few geometries at once (multi-GPU chunks render
   // different row sets in turn), least recently used replaced.
+  // An entry's buffers are stream-ordered allocations too: a replaced entry's
+  // table is freed on the launching stream behind the event of its last
+  // launch (`done`), never with a device-wide synchronisation.
   struct CostEntry {
     unsigned long long key = 0;
     unsigned* cost = nullptr;
@@ -323,6 +332,7 @@ struct rtg_context {
     int cur = 0;
     unsigned launches = 0;
     unsigned long long lastUse = 0;
+    hipEvent_t done = nullptr;  // behind the entry's last trace kernel
   };
   static constexpr int kCostEntries = 8;
   CostEntry costs[kCostEntries];
@@ -471,16 +481,21 @@ int rtg_context_destroy(rtg_context* ctx) {
   (void)hipFree(ctx->diag);
   (void)hipFree(ctx->counts);
   (void)hipFree(ctx->timeline);
+  // stream-ordered allocations (launch_trace): freed on the null stream after
+  // all work of the device that may still read them
+  (void)hipDeviceSynchronize();
   for (auto& sl : ctx->slots) {
-    (void)hipFree(sl.list);
-    (void)hipFree(sl.sel);
-    (void)hipFree(sl.count);
+    if (sl.list) (void)hipFreeAsync(sl.list, nullptr);
+    if (sl.sel) (void)hipFreeAsync(sl.sel, nullptr);
+    if (sl.count) (void)hipFreeAsync(sl.count, nullptr);
     if (sl.done) (void)hipEventDestroy(sl.done);
   }
   for (auto& ce : ctx->costs) {
-    (void)hipFree(ce.cost);
-    (void)hipFree(ce.stat);
+    if (ce.cost) (void)hipFreeAsync(ce.cost, nullptr);
+    if (ce.stat) (void)hipFreeAsync(ce.stat, nullptr);
+    if (ce.done) (void)hipEventDestroy(ce.done);
   }
+  (void)hipStreamSynchronize(nullptr);
   delete ctx;
   return RTG_OK;
 }
@@ -575,8 +590,11 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   }
   // Table limits of the kernel: a frame record keeps the refractive material
   // index in 22 bits (FrameC::meta, rm << 10), and scene tables are addressed
-  // with 32-bit byte offsets (fidx / uidx; the fused records end at 80 n
-  // bytes).  Both hold for n < RTG_MAX_SPHERES.
+  // with 32-bit byte offsets (fidx / uidx).  For n < RTG_MAX_SPHERES the
+  // per-sphere tables end below 2^32 bytes (the fused records at 80 n bytes,
+  // the BVH at < 128 n); the sphere lists, which grow as O(m n^2), are capped
+  // separately (kListMaxRecords, sphere_lists: over it a scene has no lists
+  // and its queries take the BVH).
   if (sphNum >= RTG_MAX_SPHERES) {
     rtg_set_error("rtg_context_set_scene: %u spheres (at most %u)", sphNum, RTG_MAX_SPHERES - 1);
     return RTG_ERR_INVALID;
@@ -738,9 +756,11 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   const bool sampleKernel = vi->kind == kVariantSample;
   // the default sample kernel reads materials/geometry from global memory
   // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
-  if (variant == 0 || variant == 15 || variant == 18 || variant == 19 || variant == 20 ||
-      variant == 21 || variant == 22 || variant == 23 || variant == 24 || variant == 50 ||
-      variant == 110 || variant == 120)
+  // (as do the shipped tile kernels 9, 59, 100); only the A/B variants below
+  // stage it
+  if (!(variant == 1 || variant == 2 || variant == 3 || variant == 4 || variant == 5 ||
+        variant == 6 || variant == 8 || variant == 14 || variant == 16 || variant == 17 ||
+        variant == 104 || variant == 108))
     ldsMats = false;
   unsigned rows;
   if (rowList) {
@@ -797,6 +817,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.groupCost = nullptr;
   a.costStat = nullptr;
   a.costPrev = nullptr;
+  a.zeroCount = nullptr;
+  a.zeroStat = nullptr;
+  rtg_context::CostEntry* costEntry = nullptr;  // the feedback entry of this launch
   if (variant == 120) {  // executed-work counting build
     if (!ctx->counts) {
       HIP_TRY(hipMalloc(&ctx->counts, 2 * kCntSlots * sizeof(unsigned long long)));
@@ -835,24 +858,28 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     const bool compact = tpb == 64 && variant != 21 && variant != 22;
     if (compact && ctx->n <= 64 && groups <= 0xFFFFFFFFull) {
       listed = true;
+      const hipStream_t st = (hipStream_t)stream;
       slot = &ctx->slots[ctx->nextSlot];
       ctx->nextSlot = (ctx->nextSlot + 1) % rtg_context::kSlots;
       if (!slot->done) HIP_TRY(hipEventCreateWithFlags(&slot->done, hipEventDisableTiming));
-      else HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, slot->done, 0));
+      else HIP_TRY(hipStreamWaitEvent(st, slot->done, 0));  // the slot's last launch
       if (slot->cap < groups) {
-        // the slot's last kernel must be done before its list is freed
-        HIP_TRY(hipEventSynchronize(slot->done));
-        (void)hipFree(slot->list);
-        (void)hipFree(slot->sel);
+        // stream-ordered: freed after the slot's last kernel (waited on above)
+        if (slot->list) HIP_TRY(hipFreeAsync(slot->list, st));
+        if (slot->sel) HIP_TRY(hipFreeAsync(slot->sel, st));
         slot->list = nullptr;
         slot->sel = nullptr;
         slot->cap = 0;
         // two halves of `groups` entries (the four runs, KernelArgs::groupCount)
-        HIP_TRY(hipMalloc(&slot->list, 2 * groups * sizeof(unsigned)));
-        HIP_TRY(hipMalloc(&slot->sel, 2 * groups * sizeof(unsigned long long)));
+        HIP_TRY(hipMallocAsync((void**)&slot->list, 2 * groups * sizeof(unsigned), st));
+        HIP_TRY(hipMallocAsync((void**)&slot->sel, 2 * groups * sizeof(unsigned long long), st));
         slot->cap = groups;
       }
-      if (!slot->count) HIP_TRY(hipMalloc(&slot->count, 4 * sizeof(unsigned)));
+      if (!slot->count) {
+        HIP_TRY(hipMallocAsync((void**)&slot->count, 8 * sizeof(unsigned), st));
+        HIP_TRY(hipMemsetAsync(slot->count, 0, 8 * sizeof(unsigned), st));
+        slot->parity = 0;
+      }
       if (ctx->orderFeedback && !(ctx->opts.flags & RTG_LAUNCH_NO_ORDER_FEEDBACK)) {
         // launch-order feedback: this frame geometry's entry (LRU)
         const unsigned long long key = geometry_key(width, height, zoom, aliasFactor, stackSize,
@@ -865,18 +892,24 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
           ce = &ctx->costs[0];
           for (auto& e : ctx->costs)
             if (e.lastUse < ce->lastUse) ce = &e;
+          // the replaced entry's buffers may still be read by queued launches
+          // (any stream): this stream waits for its last one
+          if (ce->done) HIP_TRY(hipStreamWaitEvent(st, ce->done, 0));
+          else HIP_TRY(hipEventCreateWithFlags(&ce->done, hipEventDisableTiming));
+          ce->key = 0;
+          ce->launches = 0;
           if (ce->cap < groups) {
-            // an evicted entry's buffers may still be read by queued launches
-            HIP_TRY(hipDeviceSynchronize());
-            (void)hipFree(ce->cost);
+            if (ce->cost) HIP_TRY(hipFreeAsync(ce->cost, st));
             ce->cost = nullptr;
             ce->cap = 0;
-            HIP_TRY(hipMalloc(&ce->cost, groups * sizeof(unsigned)));
+            HIP_TRY(hipMallocAsync((void**)&ce->cost, groups * sizeof(unsigned), st));
             ce->cap = groups;
           }
-          if (!ce->stat) HIP_TRY(hipMalloc(&ce->stat, 2 * sizeof(unsigned long long)));
+          if (!ce->stat)
+            HIP_TRY(hipMallocAsync((void**)&ce->stat, 2 * sizeof(unsigned long long), st));
+          HIP_TRY(hipMemsetAsync(ce->stat, 0, 2 * sizeof(unsigned long long), st));
+          ce->cur = 0;
           ce->key = key;
-          ce->launches = 0;
         }
         ce->lastUse = ++ctx->costClock;
         // the trace kernel writes groupCost every launch; the cull pass reads
@@ -886,7 +919,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         a.costStat = ce->launches >= 1 ? ce->stat + ce->cur : nullptr;
         a.costPrev = ce->launches >= 2 ? ce->stat + (1 - ce->cur) : nullptr;
         if (ce->launches >= 1) ce->cur = 1 - ce->cur;
+        // the next launch's costStat, zeroed by this launch's trace kernel
+        a.zeroStat = ce->stat + ce->cur;
         ++ce->launches;
+        costEntry = ce;
       }
       cullGroups = groups;  // the cull pass is enqueued below, after the last failure point
       // about one wave per listed group: the benchmark scenes list 13-17 % of
@@ -897,7 +933,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       if (ctx->persistPerCU > 0) persist = (size_t)ctx->numCU * ctx->persistPerCU;
       a.groupList = slot->list;
       a.groupSel = slot->sel;
-      a.groupCount = slot->count;
+      a.groupCount = slot->count + 4 * slot->parity;
+      a.zeroCount = slot->count + 4 * (1 - slot->parity);
+      slot->parity ^= 1u;
       a.groupCap = (unsigned)groups;  // light groups are listed from index groups - 1 down
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
       grid = dim3(a.nPersist, 1);
@@ -935,20 +973,26 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // Stream work starts here, after every check and allocation that can fail,
   // so an error never leaves a cull pass (which zero-fills dst and fills the
   // slot's list) in flight without the slot's event behind it.
+  // No memset: the counters this cull pass adds to were zeroed by the
+  // previous launch's trace kernel (KernelArgs::zeroCount / zeroStat).
   if (slot) {
-    HIP_TRY(hipMemsetAsync(slot->count, 0, 4 * sizeof(unsigned), (hipStream_t)stream));
-    if (a.costStat)
-      HIP_TRY(hipMemsetAsync(a.costStat, 0, sizeof(unsigned long long), (hipStream_t)stream));
+    const hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(
         cull_groups_kernel,
         dim3((unsigned)((cullGroups + 256 * kCullRounds - 1) / (256 * kCullRounds))), dim3(256),
-        0, (hipStream_t)stream, a, cullGroups, slot->list, slot->sel, slot->count);
-    const hipError_t e = hipGetLastError();
-    if (e == hipSuccess)
-      hipLaunchKernelGGL(fn, grid, dim3(threads), lds, (hipStream_t)stream, a);
-    (void)hipEventRecord(slot->done, (hipStream_t)stream);  // on every path
+        0, st, a, cullGroups, slot->list, slot->sel, const_cast<unsigned*>(a.groupCount));
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(fn, grid, dim3(threads), lds, st, a);
+      e = hipGetLastError();
+    }
+    if (e != hipSuccess) {  // no trace kernel zeroed the next launch's counters
+      (void)hipMemsetAsync(a.zeroCount, 0, 4 * sizeof(unsigned), st);
+      if (a.zeroStat) (void)hipMemsetAsync(a.zeroStat, 0, sizeof(unsigned long long), st);
+    }
+    (void)hipEventRecord(slot->done, st);  // on every path
+    if (costEntry) (void)hipEventRecord(costEntry->done, st);
     HIP_TRY(e);
-    HIP_TRY(hipGetLastError());
     return RTG_OK;
   }
   hipLaunchKernelGGL(fn, grid, dim3(threads), lds, (hipStream_t)stream, a);

@@ -241,13 +241,24 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
 //    (r + 1e-6f)^2, index, refractive index}.
 // capOff[l n + h] .. capOff[l n + h + 1] and ovOff[h] .. ovOff[h + 1] index
 // the records.  Empty for non-finite scenes (the queries then use the BVH).
+//
+// Limits.  The kernel addresses the record tables with 32-bit byte offsets
+// (fidx(capRec, 8k): 32 k bytes), and the lists grow as O(m n^2) records, so
+// a table is capped at kListMaxRecords records (2^23: 256 MiB, far below the
+// 2^27 records where the offsets would wrap); and building them costs
+// m n^2 capsule tests plus n^2 overlap tests, so scenes where that exceeds
+// kListMaxTests get no lists.  Either way the tables stay empty, has_lists()
+// is false and every query takes the BVH (same answers, slower).
 constexpr int kListWords = 8;
+constexpr size_t kListMaxRecords = size_t(1) << 23;
+constexpr double kListMaxTests = 0x1p28;
 inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
-                         unsigned m, PackedScene* ps) {
+                         unsigned m, PackedScene* ps, size_t maxRecords = kListMaxRecords) {
   ps->capRec.clear();
   ps->capOff.clear();
   ps->ovRec.clear();
   ps->ovOff.clear();
+  if ((double)(m + 1) * n * n > kListMaxTests) return;
   auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
   for (unsigned i = 0; i < n; ++i)
     if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
@@ -293,15 +304,27 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
     pool.emplace_back(work, (unsigned)((size_t)total * t / nt),
                       (unsigned)((size_t)total * (t + 1) / nt));
   for (auto& th : pool) th.join();
+  size_t capTotal = 0;
+  for (const auto& l : lists) capTotal += l.size();
+  if (capTotal + 1 > maxRecords) return;  // (+1: the padding record)
+  std::vector<std::vector<unsigned>> ov(n);
+  size_t ovTotal = 0;
+  for (unsigned h = 0; h < n; ++h) {
+    for (unsigned j = 0; j < n; ++j)
+      if (overlap_keep(spheres, h, j)) ov[h].push_back(j);
+    ovTotal += ov[h].size();
+    if (ovTotal + 1 > maxRecords) return;
+  }
+  ps->capRec.reserve((capTotal + 1) * kListWords);
   ps->capOff.push_back(0);
   for (unsigned q = 0; q < total; ++q) {
     for (unsigned i : lists[q]) rec(ps->capRec, i);
     ps->capOff.push_back((unsigned)(ps->capRec.size() / kListWords));
   }
+  ps->ovRec.reserve((ovTotal + 1) * kListWords);
   ps->ovOff.push_back(0);
   for (unsigned h = 0; h < n; ++h) {
-    for (unsigned j = 0; j < n; ++j)
-      if (overlap_keep(spheres, h, j)) rec(ps->ovRec, j);
+    for (unsigned j : ov[h]) rec(ps->ovRec, j);
     ps->ovOff.push_back((unsigned)(ps->ovRec.size() / kListWords));
   }
   // one padding record past each table's end: the kernel reads records in
@@ -417,8 +440,8 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
 // Top-down: a node's spheres are split in two by a surface-area sweep (split
 // below), and each half again, into four groups; a group of one sphere
 // becomes a sphere slot, a larger group a child node; nodes of <= 4 spheres
-// hold sphere slots only.  Returns false (no BVH) for non-finite scenes or an
-// implausibly deep tree.
+// hold sphere slots only.  Returns false (no BVH) for non-finite scenes,
+// coordinates beyond 2^56 or an implausibly deep tree.
 inline float round_up_f(double v) {
   float f = (float)v;
   if ((double)f < v) f = nextafterf(f, __builtin_inff());
@@ -490,6 +513,11 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
         !finite(spheres[i].radius))
       return false;
   const OriginBox ob = origin_box(spheres, n);
+  // The slab test (rtg_trace.h make_boxq / slab_pass) multiplies origins and
+  // box planes by 1/d, up to 2^64 for a near-axis direction: with every
+  // coordinate below 2^57 (the origin box and the grown boxes within it) the
+  // products stay below 2^121, finite.  Larger scenes take the flat queries.
+  if (!(ob.omax <= 0x1p56)) return false;
   // grown boxes: 6 floats per sphere
   std::vector<float> gb((size_t)n * 6);
   for (unsigned i = 0; i < n; ++i) {

@@ -524,6 +524,14 @@ struct KernelArgs {
   unsigned* groupCost;
   unsigned long long* costStat;        // this cull pass's sums (zeroed before it), or null
   const unsigned long long* costPrev;  // the previous cull pass's, or null
+  // Counters of the NEXT launch that this launch's trace kernel zeroes (its
+  // first wave, lane 0), so that no memset precedes a cull pass: the slot's
+  // other group-count set ([4]) and the cost entry's next costStat (or null).
+  // Neither is in use while this launch's trace runs: the slot's previous
+  // launch is complete (its event), and this launch's cull pass has read its
+  // costPrev before the trace starts (one stream).
+  unsigned* zeroCount;
+  unsigned long long* zeroStat;
   unsigned long long* diag;  // kProbeSlots counters (diagnostic variants only)
   unsigned long long* counts;  // 2 x kCntSlots unit counters (counting build, variant 120)
   uint4* timeline;           // per-wave records (RTG_LAUNCH_TIMELINE) or null
@@ -985,6 +993,12 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
                       : ~0u;
     };
     record_wave_start(a, t0, gw);
+    if (gw == 0 && (threadIdx.x & 63u) == 0) {  // the next launch's counters (KernelArgs)
+      const RTG_CONST KernelArgs* b = kargs();
+      unsigned* zc = b->zeroCount;
+      zc[0] = zc[1] = zc[2] = zc[3] = 0u;
+      if (unsigned long long* zs = b->zeroStat) *zs = 0ull;
+    }
     unsigned tg = t0;  // this group's start (the first one's includes the wave's set-up)
     for (unsigned idx = (unsigned)gw;; idx += kargs()->nPersist) {
       const unsigned at = pos(idx);
@@ -1090,17 +1104,27 @@ struct VariantInfo {
   int kind;
   bool semantic;
 };
+// The shipped library holds the default kernel (0), its tile fallback for
+// nAA > 8 (9), the OpenCL-semantics forms (50, 59), the diagnostic builds of
+// 9 and 0 (100, 110) and the counting build (120).  The A/B variants, each
+// measured and not adopted, are compiled only into A/B
+// libraries (`make AB=1`, -DRTG_AB_VARIANTS=1).
+#ifndef RTG_AB_VARIANTS
+#define RTG_AB_VARIANTS 0
+#endif
 constexpr VariantInfo kVariants[] = {
-    {0, kVariantSample, false},  {1, kVariantTile, false},    {2, kVariantTile, false},
-    {3, kVariantTile, false},    {4, kVariantTile, false},    {5, kVariantTile, false},
-    {6, kVariantTile, false},    {8, kVariantTile, false},    {9, kVariantTile, false},
-    {14, kVariantSample, false}, {15, kVariantSample, false}, {16, kVariantSample, false},
-    {17, kVariantSample, false}, {18, kVariantSample, false}, {19, kVariantSample, false},
-    {20, kVariantSample, false}, {21, kVariantSample, false}, {22, kVariantSample, false},
-    {23, kVariantSample, false}, {24, kVariantSample, false},
-    {50, kVariantSample, true},  {59, kVariantTile, true},    {100, kVariantTile, false},
-    {104, kVariantTile, false},  {108, kVariantTile, false},  {110, kVariantSample, false},
+    {0, kVariantSample, false},  {9, kVariantTile, false},    {50, kVariantSample, true},
+    {59, kVariantTile, true},    {100, kVariantTile, false},  {110, kVariantSample, false},
     {120, kVariantSample, false},
+#if RTG_AB_VARIANTS
+    {1, kVariantTile, false},    {2, kVariantTile, false},    {3, kVariantTile, false},
+    {4, kVariantTile, false},    {5, kVariantTile, false},    {6, kVariantTile, false},
+    {8, kVariantTile, false},    {14, kVariantSample, false}, {15, kVariantSample, false},
+    {16, kVariantSample, false}, {17, kVariantSample, false}, {18, kVariantSample, false},
+    {19, kVariantSample, false}, {20, kVariantSample, false}, {21, kVariantSample, false},
+    {22, kVariantSample, false}, {23, kVariantSample, false}, {24, kVariantSample, false},
+    {104, kVariantTile, false},  {108, kVariantTile, false},
+#endif
 };
 inline const VariantInfo* variant_info(int v) {
   for (const VariantInfo& i : kVariants)
@@ -1123,17 +1147,18 @@ template <int S, int V>
 static TraceFn trace_fn_v(bool lds, int list) {
   if (list && !CompactVariant<V>::value) return nullptr;
   if constexpr (V == 0) {
+    // S <= 6: the SGPR-budgeted 8-wave kernel; deeper stacks hold more LDS
+    // per wave than 8 waves per SIMD admit anyway
     if (list == 2) {
-      // S <= 6: the SGPR-budgeted 8-wave kernel; deeper stacks hold more LDS
-      // per wave than 8 waves per SIMD admit anyway
       if constexpr (S <= 6) return trace_samples_kernel_masked<S>;
       else return trace_samples_kernel<S, false, 0, false, true, true>;
     }
-  }
-  if constexpr (V == 120) {  // the counting build of exactly that kernel
-    if (list == 2) return trace_samples_kernel<S, false, 120, false, true, true>;
-  }
-  if constexpr (V == 17) {
+    return list ? trace_samples_kernel<S, false, 0, false, true> : trace_samples_kernel<S, false, 0>;
+  } else if constexpr (V == 120) {  // the counting build of exactly the masked kernel
+    return list == 2 ? trace_samples_kernel<S, false, 120, false, true, true> : nullptr;
+  } else if constexpr (V == 110) {  // the probe build of the compacted default kernel
+    return list ? trace_samples_kernel<S, false, 110, false, true> : nullptr;
+  } else if constexpr (V == 17) {
     if (list)
       return lds ? trace_samples_kernel<S, true, V, false, true>
                  : trace_samples_kernel<S, false, V, false, true>;
@@ -1144,29 +1169,30 @@ static TraceFn trace_fn_v(bool lds, int list) {
     return list ? trace_samples_kernel<S, false, V, false, true> : trace_samples_kernel<S, false, V>;
   } else if constexpr (V == 21 || V == 22) {
     return trace_samples_kernel<S, false, V>;
+  } else if constexpr (V == 9 || V == 59 || V == 100) {
+    (void)lds;  // the shipped tile kernels read the scene from global memory
+    return trace_kernel<S, false, V>;
   } else {
     return lds ? trace_kernel<S, true, V> : trace_kernel<S, false, V>;
   }
 }
 // BVH scenes: the default kernels (and their diagnostic and OpenCL-semantics
-// forms) have kBvh instantiations; other A/B variants run BVH scenes through
-// their flat queries (same results, slower).  The launcher sizes a kBvh
+// forms, the counting build) and the nAA > 8 tile fallback have kBvh
+// instantiations; 59, 100 and the A/B variants run BVH scenes through their
+// flat queries (same results, slower); the probe build 110 has none (an
+// error on BVH scenes).  The launcher sizes a kBvh
 // kernel's LDS by frame_lds_levels(S, true), so this list and
 // has_bvh_kernel() must agree.
 inline bool has_bvh_kernel(int variant) {
-  return variant == 0 || variant == 50 || variant == 110 || variant == 120 || variant == 9 ||
-         variant == 59 || variant == 100;
+  return variant == 0 || variant == 50 || variant == 120 || variant == 9;
 }
 template <int S>
 static TraceFn trace_fn_bvh(bool lds, int variant) {
   switch (variant) {
     case 0: return trace_samples_kernel<S, false, 0, true>;
     case 50: return trace_samples_kernel<S, false, 50, true>;
-    case 110: return trace_samples_kernel<S, false, 110, true>;
     case 120: return trace_samples_kernel<S, false, 120, true>;
-    case 9: return lds ? trace_kernel<S, true, 9, true> : trace_kernel<S, false, 9, true>;
-    case 59: return lds ? trace_kernel<S, true, 59, true> : trace_kernel<S, false, 59, true>;
-    case 100: return lds ? trace_kernel<S, true, 100, true> : trace_kernel<S, false, 100, true>;
+    case 9: (void)lds; return trace_kernel<S, false, 9, true>;
     default: return nullptr;
   }
 }
@@ -1177,9 +1203,25 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh, int list) {
     if (TraceFn f = trace_fn_bvh<S>(lds, variant)) return f;
   }
   switch (variant) {
+    case 0: return trace_fn_v<S, 0>(lds, list);
+    case 9: return trace_fn_v<S, 9>(lds, list);
+    case 50: return trace_fn_v<S, 50>(lds, list);
+    case 59: return trace_fn_v<S, 59>(lds, list);
     case 100: return trace_fn_v<S, 100>(lds, list);
     case 110: return trace_fn_v<S, 110>(lds, list);
     case 120: return trace_fn_v<S, 120>(lds, list);
+#if RTG_AB_VARIANTS
+    case 1: return trace_fn_v<S, 1>(lds, list);
+    case 2: return trace_fn_v<S, 2>(lds, list);
+    case 3: return trace_fn_v<S, 3>(lds, list);
+    case 4: return trace_fn_v<S, 4>(lds, list);
+    case 5: return trace_fn_v<S, 5>(lds, list);
+    case 6: return trace_fn_v<S, 6>(lds, list);
+    case 8: return trace_fn_v<S, 8>(lds, list);
+    case 14: return trace_fn_v<S, 14>(lds, list);
+    case 15: return trace_fn_v<S, 15>(lds, list);
+    case 16: return trace_fn_v<S, 16>(lds, list);
+    case 17: return trace_fn_v<S, 17>(lds, list);
     case 18: return trace_fn_v<S, 18>(lds, list);
     case 19: return trace_fn_v<S, 19>(lds, list);
     case 20: return trace_fn_v<S, 20>(lds, list);
@@ -1187,23 +1229,9 @@ static TraceFn trace_fn(bool lds, int variant, bool bvh, int list) {
     case 22: return trace_fn_v<S, 22>(lds, list);
     case 23: return trace_fn_v<S, 23>(lds, list);
     case 24: return trace_fn_v<S, 24>(lds, list);
-    case 50: return trace_fn_v<S, 50>(lds, list);
-    case 59: return trace_fn_v<S, 59>(lds, list);
     case 104: return trace_fn_v<S, 104>(lds, list);
-    case 1: return trace_fn_v<S, 1>(lds, list);
-    case 4: return trace_fn_v<S, 4>(lds, list);
-    case 5: return trace_fn_v<S, 5>(lds, list);
-    case 6: return trace_fn_v<S, 6>(lds, list);
-    case 8: return trace_fn_v<S, 8>(lds, list);
-    case 9: return trace_fn_v<S, 9>(lds, list);
-    case 14: return trace_fn_v<S, 14>(lds, list);
-    case 15: return trace_fn_v<S, 15>(lds, list);
-    case 16: return trace_fn_v<S, 16>(lds, list);
-    case 17: return trace_fn_v<S, 17>(lds, list);
     case 108: return trace_fn_v<S, 108>(lds, list);
-    case 2: return trace_fn_v<S, 2>(lds, list);
-    case 3: return trace_fn_v<S, 3>(lds, list);
-    case 0: return trace_fn_v<S, 0>(lds, list);
+#endif
     default: return nullptr;  // not in kVariants
   }
 }

@@ -813,3 +813,19 @@ extern "C" long hostsim_cone_mask_check(long scenes, unsigned n, long rays,
   if (tested) *tested = cnt;
   return bad;
 }
+
+// Sphere-list sizes of a scene (sphere_lists, rtg_scene_pack.h) under a
+// record budget: out = {capsule records, overlap records, BVH nodes} (0, 0 when
+// the scene gets no lists: over the budget or the build-cost threshold).
+extern "C" void hostsim_list_records(const rtg_sphere* spheres, unsigned n,
+                                     const rtg_light* lights, unsigned m,
+                                     unsigned long long maxRecords, unsigned long long* out) {
+  rtg::PackedScene ps;
+  out[0] = out[1] = out[2] = 0;
+  if (!rtg::build_bvh(spheres, n, &ps)) return;
+  out[2] = ps.bvhNodes.size() / rtg::kBvhWords;
+  rtg::sphere_lists(spheres, n, lights, m, &ps, (size_t)maxRecords);
+  if (ps.capOff.empty()) return;
+  out[0] = ps.capRec.size() / rtg::kListWords - 1;  // without the padding record
+  out[1] = ps.ovRec.size() / rtg::kListWords - 1;
+}

@@ -18,6 +18,10 @@ from conftest import (GOLDEN, bits_equal, canon_md5, first_mismatch, load_f32, l
 pytestmark = pytest.mark.gpu
 
 ALL = ["ref800", "c1", "c2", "c3", "c4", "c5"]
+# Kernel variants of the shipped librtg.so (rtg_trace_kernels.h kVariants);
+# the A/B variants exist only in `make AB=1` builds (test_ab_variants).
+SHIPPED = [0, 9, 100, 110, 120]
+AB_VARIANTS = [1, 2, 3, 4, 5, 6, 8, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 104, 108]
 
 
 @pytest.fixture(scope="module")
@@ -137,16 +141,11 @@ def test_random_scenes_vs_oracle(R, oracle):
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
 
 
-@pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23, 24])
-def test_random_scenes_vs_oracle_variants(R, oracle, torch_cuda, variant):
-    """Mapping variants over random scenes, sizes and alias factors (the
-    sample-parallel kernel packs 64 // nAA^2 pixels per wave and falls back to
-    the default kernel above nAA = 8)."""
-    torch = torch_cuda
+def _random_vs_oracle(R, oracle, torch, variant, trials=16):
     rng = np.random.default_rng(77 + variant)
     ctx = R.Context(0)
     ctx.set_variant(variant)
-    for trial in range(16):
+    for trial in range(trials):
         S = int(rng.integers(1, 17))
         n, m = int(rng.integers(0, 20)), int(rng.integers(0, 5))
         W, H = int(rng.integers(1, 70)), int(rng.integers(1, 50))
@@ -163,6 +162,64 @@ def test_random_scenes_vs_oracle_variants(R, oracle, torch_cuda, variant):
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         assert bits_equal(got, want), (trial, S, n, m, W, H, aa, first_mismatch(got, want))
+    ctx.close()
+
+
+@pytest.mark.parametrize("variant", [0, 9])
+def test_random_scenes_vs_oracle_variants(R, oracle, torch_cuda, variant):
+    """The sample kernel and the tile kernel over random scenes, sizes and
+    alias factors (the sample-parallel kernel packs 64 // nAA^2 pixels per
+    wave and falls back to the tile kernel above nAA = 8)."""
+    _random_vs_oracle(R, oracle, torch_cuda, variant)
+
+
+def clustered_scene(rng, n, m, refr_frac=0.5):
+    """A BVH-scale scene (n > 64): spheres packed in a few overlapping
+    clusters, many of them refractive, several lights, so that the coherent
+    waves take the sphere lists (capsule / overlap lists) and the incoherent
+    ones the BVH queries."""
+    import rtg_amd as R
+    sph = np.zeros(n, R.SPHERE_DTYPE)
+    k = int(rng.integers(2, 5))
+    ctr = np.stack([rng.uniform(-8, 8, k), rng.uniform(-5, 5, k), rng.uniform(-30, -10, k)], 1)
+    for i in range(n):
+        c = ctr[int(rng.integers(0, k))]
+        sph[i]["pos"] = c + rng.normal(0, 3.0, 3)
+        sph[i]["radius"] = rng.uniform(0.2, 1.6)
+        op = 0.0 if rng.uniform() < refr_frac else float(rng.choice([0.6, 0.8, 1.0]))
+        sph[i]["material"] = R.make_material(
+            op, float(rng.uniform(0, 1)), rng.uniform(0, 1, 3), rng.uniform(0, 1, 3),
+            float(rng.choice([1.0, 1.33, 1.55, 2.4])))
+    lg = np.zeros(m, R.LIGHT_DTYPE)
+    for l in range(m):
+        lg[l]["pos"] = [rng.uniform(-60, 60), rng.uniform(-20, 80), rng.uniform(-40, 90)]
+        lg[l]["col"] = rng.uniform(0.2, 1, 3)
+    return sph, lg
+
+
+def test_random_bvh_scenes_vs_oracle(R, oracle, torch_cuda):
+    """BVH scenes (65..400 spheres) against the oracle: clustered, overlapping
+    and refractive spheres under several lights, so the device-only list
+    paths (blocked_cap, closest_enter_list, container_list, their paired
+    record loads and padding records) and their BVH fallbacks all run."""
+    torch = torch_cuda
+    rng = np.random.default_rng(4242)
+    ctx = R.Context(0)
+    for trial in range(10):
+        n, m = int(rng.integers(65, 401)), int(rng.integers(1, 5))
+        S = int(rng.choice([3, 6, 8, 10]))
+        W, H = int(rng.integers(24, 72)), int(rng.integers(16, 48))
+        aa = float(rng.choice([1.0, 3.0]))
+        sph, lg = clustered_scene(rng, n, m)
+        want = oracle.render(sph, lg, W, H, S, aa=aa)
+        ctx.set_scene(sph, lg)
+        assert ctx.scene_stats()["bvh_nodes"] > 0, (trial, n)
+        out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        ctx.render_device(W, H, out.data_ptr(), alias_factor=aa, stack_size=S,
+                          stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert bits_equal(got, want), (trial, n, m, S, W, H, aa, first_mismatch(got, want))
     ctx.close()
 
 
@@ -293,7 +350,7 @@ def test_launch_order_feedback_keeps_frames(R, golden, torch_cuda):
     ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 9, 14, 15, 17, 18, 20, 21, 22, 23, 24])
+@pytest.mark.parametrize("variant", [0, 9])
 def test_variant_full_frames(R, golden, torch_cuda, variant):
     """Kernel mappings over whole frames, sharded frames, row lists and
     back-to-back launches on two streams."""
@@ -380,13 +437,10 @@ def test_errors_are_returned_not_fatal(R):
     assert fb.shape == (8, 8, 3)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 8, 9, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 100, 108, 110, 120])
-def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
-    """Every kernel variant (rtg_launch_opts.variant) is bit-exact too."""
-    torch = torch_cuda
+def _variant_small_frames(R, golden, torch, variant, names=("ref800", "c2", "c3", "c5")):
     ctx = R.Context(0)
     ctx.set_variant(variant)
-    for name in ["ref800", "c2", "c3", "c5"]:
+    for name in names:
         c = golden["configs"][name]
         sph, lg = load_scene(name, c["spheres"], c["lights"])
         sw, sh = c["small"]["W"], c["small"]["H"]
@@ -399,6 +453,46 @@ def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
         got = out.cpu().numpy()
         assert bits_equal(got, want), (name, variant, first_mismatch(got, want))
     ctx.close()
+
+
+@pytest.mark.parametrize("variant", SHIPPED)
+def test_kernel_variants_small_frames(R, golden, torch_cuda, variant):
+    """Every shipped kernel variant (rtg_launch_opts.variant) is bit-exact
+    too.  The probe build 110 has no BVH instantiation: on a BVH scene it
+    returns an error instead of a frame."""
+    if variant == 110:
+        _variant_small_frames(R, golden, torch_cuda, variant, ("ref800", "c2", "c3"))
+        c = golden["configs"]["c5"]
+        sph, lg = load_scene("c5", c["spheres"], c["lights"])
+        ctx = R.Context(0)
+        ctx.set_variant(110)
+        ctx.set_scene(sph, lg)
+        out = torch_cuda.empty((8, 8, 3), dtype=torch_cuda.float32, device="cuda")
+        with pytest.raises(R.RtgError):
+            ctx.render_device(8, 8, out.data_ptr(), stack_size=c["stack_size"])
+        ctx.close()
+    else:
+        _variant_small_frames(R, golden, torch_cuda, variant)
+
+
+def test_ab_variants(R, golden, oracle, torch_cuda):
+    """The A/B kernel variants (measured, not adopted) of a `make AB=1`
+    library: small frames and random scenes.  The shipped library leaves them
+    out, and rejects them."""
+    ctx = R.Context(0)
+    built = []
+    for v in AB_VARIANTS:
+        try:
+            ctx.set_variant(v)
+            built.append(v)
+        except R.RtgError:
+            pass
+    ctx.close()
+    if not built:
+        pytest.skip("A/B variants not built (make AB=1)")
+    for v in built:
+        _variant_small_frames(R, golden, torch_cuda, v)
+        _random_vs_oracle(R, oracle, torch_cuda, v, trials=6)
 
 
 def test_counting_build(R, golden, torch_cuda):
@@ -443,7 +537,7 @@ def test_counting_build(R, golden, torch_cuda):
     ctx.close()
 
 
-@pytest.mark.parametrize("variant", [9, 22, 0])
+@pytest.mark.parametrize("variant", [9, 0])
 def test_wave_timeline_diagnostic(R, golden, torch_cuda, variant):
     """RTG_LAUNCH_TIMELINE: one record per wave, output unchanged."""
     torch = torch_cuda
@@ -462,8 +556,6 @@ def test_wave_timeline_diagnostic(R, golden, torch_cuda, variant):
     groups = -(-(W * H) // 7)
     if variant == 9:
         assert len(rec) == ((W + 15) // 16) * ((H + 15) // 16) * 4
-    elif variant == 22:  # one wave per pixel group
-        assert len(rec) == groups
     else:  # compacted launch: about one wave per listed group
         assert 0 < len(rec) <= groups
         pc, grp = (rec[:, 3] >> 4) & 127, rec[:, 3] >> 11  # tag: first group's mask, index

@@ -397,6 +397,62 @@ def test_kernel_traversal_bvh_random_scenes(hostsim, oracle):
         assert bits_equal(got, want), (trial, S, n, m, W, H, first_mismatch(got, want))
 
 
+def test_sphere_list_limits(hostsim, golden, rtg):
+    """Sphere lists (sphere_lists, rtg_scene_pack.h) stay within their record
+    budget, whose 32-byte records the kernel addresses with 32-bit byte
+    offsets: a scene over the budget gets no lists at all (its queries take
+    the BVH), and so does a scene whose list build would cost more than the
+    threshold of capsule + overlap tests, without doing that work."""
+    import time
+    f = hostsim.hostsim_list_records
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_uint,
+                  ctypes.c_ulonglong, ctypes.c_void_p]
+    out = (ctypes.c_ulonglong * 3)()
+    c = golden["configs"]["c5"]
+    sph, lg = load_scene("c5", c["spheres"], c["lights"])
+    f(P(sph), len(sph), P(lg), len(lg), 1 << 23, out)
+    cap, ov, nodes = list(out)
+    assert cap > 0 and ov > 0 and nodes > 0, list(out)
+    assert (cap + 1) * 32 < 2 ** 32 and (ov + 1) * 32 < 2 ** 32
+    budget = max(cap, ov)  # the larger table just over the budget: no lists
+    f(P(sph), len(sph), P(lg), len(lg), budget, out)
+    assert out[0] == 0 and out[1] == 0 and out[2] == nodes
+    f(P(sph), len(sph), P(lg), len(lg), budget + 1, out)
+    assert (out[0], out[1]) == (cap, ov)
+    # (m + 1) n^2 > 2^28 tests: no lists, and no quadratic build
+    rng = np.random.default_rng(8)
+    big, lg4 = random_scene(rng, 9000, 4)
+    big["radius"] *= 0.05
+    t0 = time.time()
+    f(P(big), len(big), P(lg4), len(lg4), 1 << 23, out)
+    assert out[0] == 0 and out[1] == 0 and out[2] > 0
+    assert time.time() - t0 < 20
+
+
+def test_bvh_large_coordinates(hostsim, oracle):
+    """The slab test multiplies by 1/d (up to 2^64 for a near-axis direction):
+    scenes with coordinates up to 2^56 keep the BVH and stay bit-exact with
+    axis-aligned rays (the frame's centre column and row); beyond that the
+    scene has no BVH (flat queries, same answers)."""
+    f = hostsim.hostsim_list_records
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p, ctypes.c_uint,
+                  ctypes.c_ulonglong, ctypes.c_void_p]
+    out = (ctypes.c_ulonglong * 3)()
+    rng = np.random.default_rng(56)
+    hostsim.hostsim_set_variant(0)
+    for scale, has_bvh in ((2.0 ** 40, True), (2.0 ** 52, True), (2.0 ** 60, False)):
+        sph, lg = random_scene(rng, 80, 2)
+        sph["pos"] *= scale / 40.0
+        sph["radius"] *= scale / 40.0
+        lg["pos"] *= scale / 40.0
+        f(P(sph), len(sph), P(lg), len(lg), 1 << 23, out)
+        assert (out[2] > 0) == has_bvh, (scale, list(out))
+        W, H = 9, 7  # odd: the centre column and row have d.x = 0 / d.y = 0 samples
+        want = oracle.render(sph, lg, W, H, 4)
+        got = _hostsim_render(hostsim, sph, lg, W, H, 4)
+        assert bits_equal(got, want), (scale, first_mismatch(got, want))
+
+
 def test_cone_masks_are_conservative(hostsim):
     """Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): a sphere left
     out of mask (h, cell(U)) is never hit, by the reference's own root test,
