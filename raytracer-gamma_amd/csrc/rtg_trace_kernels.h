@@ -22,6 +22,10 @@
 namespace rtg {
 
 constexpr int kBlock = 256;
+
+#ifndef RTG_BVH_LOAD2  // A/B builds: DevScene::bvh_rec's paired node loads
+#define RTG_BVH_LOAD2 0
+#endif
 // Materials staged in LDS when the table fits (n+1 records of 32 B).
 constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 
@@ -298,10 +302,23 @@ struct DevScene {
     return list_rec(ovRec, k, rs, r2, cr, idx, rf);
   }
   // Node nd's record (BvhRec, rtg_trace.h): two 64-byte scalar loads.
+  // RTG_BVH_LOAD2 (A/B builds): both issued back to back in one asm block
+  // with one wait, into disjoint registers (the compiler's own schedule waits
+  // for the first before issuing the second: two round trips per node).
   __device__ __forceinline__ void bvh_rec(unsigned nd, BvhRec& r) const {
     typedef float f16 __attribute__((ext_vector_type(16)));
+#if RTG_BVH_LOAD2
+    f16 a, b;
+    asm volatile(
+        "s_load_dwordx16 %0, %2, %3\n\t"
+        "s_load_dwordx16 %1, %2, %3 offset:0x40\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(a), "=&s"(b)
+        : "s"(bvhNodes), "s"(nd * (unsigned)(kBvhWords * 4)));
+#else
     const RTG_CONST f16* p = (const RTG_CONST f16*)fidx(bvhNodes, kBvhWords * nd);
     const f16 a = p[0], b = p[1];
+#endif
 #pragma unroll
     for (int k = 0; k < 16; ++k) r.s[k] = a[k];
 #pragma unroll
@@ -1184,7 +1201,8 @@ static TraceFn trace_fn_v(bool lds, int list) {
 // kernel's LDS by frame_lds_levels(S, true), so this list and
 // has_bvh_kernel() must agree.
 inline bool has_bvh_kernel(int variant) {
-  return variant == 0 || variant == 50 || variant == 120 || variant == 9;
+  return variant == 0 || variant == 50 || variant == 120 || variant == 9 ||
+         (RTG_AB_VARIANTS && variant == 110);
 }
 template <int S>
 static TraceFn trace_fn_bvh(bool lds, int variant) {
@@ -1193,6 +1211,9 @@ static TraceFn trace_fn_bvh(bool lds, int variant) {
     case 50: return trace_samples_kernel<S, false, 50, true>;
     case 120: return trace_samples_kernel<S, false, 120, true>;
     case 9: (void)lds; return trace_kernel<S, false, 9, true>;
+#if RTG_AB_VARIANTS
+    case 110: return trace_samples_kernel<S, false, 110, true>;  // probe build, A/B libraries
+#endif
     default: return nullptr;
   }
 }
