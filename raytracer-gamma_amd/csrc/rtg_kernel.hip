@@ -294,6 +294,8 @@ struct rtg_context {
   unsigned* capOff = nullptr;
   float* ovRec = nullptr;
   unsigned* ovOff = nullptr;
+  float* nbrRec = nullptr;    // neighbour lists of BVH scenes (null when none)
+  unsigned* nbrOff = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   unsigned long long* counts = nullptr;  // unit counters of the counting build (variant 120)
@@ -368,6 +370,10 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->capOff);
   (void)hipFree(c->ovRec);
   (void)hipFree(c->ovOff);
+  (void)hipFree(c->nbrRec);
+  (void)hipFree(c->nbrOff);
+  c->nbrRec = nullptr;
+  c->nbrOff = nullptr;
   c->capRec = nullptr;
   c->capOff = nullptr;
   c->ovRec = nullptr;
@@ -678,6 +684,18 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->ovOff, ps.ovOff.data(), ps.ovOff.size() * sizeof(unsigned),
                       hipMemcpyHostToDevice));
   }
+  if (!ps.nbrOff.empty()) {
+    if (hipMalloc(&ctx->nbrRec, ps.nbrRec.size() * sizeof(float)) != hipSuccess ||
+        hipMalloc(&ctx->nbrOff, ps.nbrOff.size() * sizeof(unsigned)) != hipSuccess) {
+      free_scene(ctx);
+      rtg_set_error("hipMalloc failed for the neighbour lists");
+      return RTG_ERR_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(ctx->nbrRec, ps.nbrRec.data(), ps.nbrRec.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(ctx->nbrOff, ps.nbrOff.data(), ps.nbrOff.size() * sizeof(unsigned),
+                      hipMemcpyHostToDevice));
+  }
   ctx->n = sphNum;
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
@@ -688,10 +706,10 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   ctx->sceneStats[1] = std::chrono::duration<double, std::milli>(tEnd - tUp).count();
   ctx->sceneStats[2] = (double)((ps.geom.size() + ps.crad2.size() + ps.mats.size() +
                                  ps.lights.size() + ps.prim.size() + ps.bvhNodes.size() +
-                                 ps.capRec.size() + ps.ovRec.size()) *
+                                 ps.capRec.size() + ps.ovRec.size() + ps.nbrRec.size()) *
                                     sizeof(float) +
                                 (ps.smask.size() + ps.cone.size() + ps.capOff.size() +
-                                 ps.ovOff.size()) *
+                                 ps.ovOff.size() + ps.nbrOff.size()) *
                                     sizeof(unsigned));
   ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / kBvhWords);
   return RTG_OK;
@@ -793,6 +811,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.capOff = ctx->capOff;
   a.ovRec = ctx->ovRec;
   a.ovOff = ctx->ovOff;
+  a.nbrRec = ctx->nbrRec;
+  a.nbrOff = ctx->nbrOff;
   a.n = ctx->n;
   a.m = ctx->m;
   a.n4 = ctx->n4;

@@ -233,6 +233,7 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kUDiagEnterSame, // (diagnostic) ... the same sphere
              kUDiagContSame,  // (diagnostic) refraction target query, one hit sphere
              kULightDir,    // matte_light: a light no facing-away test excluded (direction)
+             kUNbrIter,     // closest_near: one neighbour-list sphere (certificate, screen)
              kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
@@ -297,6 +298,12 @@ struct Frame {
 // prices that traffic.
 #ifndef RTG_SCRATCH_X2
 #define RTG_SCRATCH_X2 0
+#endif
+// BVH scenes: refraction children that leave their sphere take
+// closest_near over the neighbour lists (1; an A/B build: measured in the
+// host build at about 1 % less executed work on C5).
+#ifndef RTG_SEED_EXIT
+#define RTG_SEED_EXIT 0
 #endif
 struct RayQ {
   V3 o, d;
@@ -818,6 +825,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
   int rm = (int)sc.n;                   // background material
   int enterH = -1;  // Q == 4: the sphere this ray entered (refraction child), or -1
   int originH = -1;  // Q == 4: the sphere whose origin ball holds this ray's origin, or -1
+  int exitH = -1;    // Q == 4, RTG_SEED_EXIT: the sphere this ray leaves (closest_seeded), or -1
 #if defined(__HIP_DEVICE_COMPILE__) && (defined(RTG_PAD_SALU) || defined(RTG_PAD_VALU))
   unsigned padS;  // issue-cost probes (A/B builds only): dummy work per node
   float padV;
@@ -876,6 +884,12 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       sc.count(kUQuery, 1);
       hit = closest_enter_list(sc, make_query(o, d), sc.first_lane_i(enterH), t, ok);
       if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
+    } else if (RTG_SEED_EXIT && Q == 4 && sc.has_nbr() && sc.all(exitH >= 0) &&
+               sc.all(sc.first_lane_i(exitH) == exitH)) {
+      // BVH scene, coherent wave of rays from one sphere's origin ball: its
+      // neighbour list, then the BVH for the lanes it does not certify
+      sc.count(kUQuery, 1);
+      hit = closest_near(sc, make_query(o, d), sc.first_lane_i(exitH), t);
     } else {
       if (sc.has_bvh() && sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
       sc.count(kCntFullQ, 1);
@@ -883,6 +897,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     }
     enterH = -1;
     originH = -1;
+    exitH = -1;
     sc.probe_end(kProbeClosest);
     sc.probe_begin(kProbeShade);
     if (hit < 0) {
@@ -969,6 +984,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           // refraction child: calculateRefraction's refracted ray (:805-809);
           // hit from outside (cosA1 < 0): the child starts in sphere `hit`
           if (Q == 4 && vdot(d, N) < 0.f) enterH = hit;
+          else if (RTG_SEED_EXIT && Q == 4 && guardOK) exitH = hit;  // leaves hit from P
           if (Q == 4 && guardOK && sc.has_cone()) originH = hit;  // the child starts at P
           I = vsmul((1.f - R), vsmul(tr, I));
           o = P;
@@ -1139,6 +1155,39 @@ RTG_HD float pass1_rad(const RayQ& q, V3 c, float rs) {
   const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
   const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rs)));
   return fmaf(x, x, fmaf(-q.ap, cs, 0x1p-100f));
+}
+
+// Spheres wholly behind the ray's origin.  The reference accepts no root of
+// sphere i (raytracer.h:105-138) when its b = 2 d.p > 0 and c = |p|^2 - r^2
+// >= 0 (the origin outside, the centre ahead of it along -d) with b < 150 a:
+// then radicand <= fl(b b) so root <= b (1 + 2^-23), -b + root <= 2^-23 b
+// (exact, Sterbenz), u0 <= 2^-23 b / 2a (1 + 2^-24) < 9e-6 < 1e-5, and u1 < 0.
+// `behind` proves those from the pass-1 screen's fused terms (p exactly the
+// reference's, x = d.p and cs = |p|^2 - rs fused, rs >= r^2):
+//  * x > 2^-20 (a + cs + rs): the reference's d.p and the fused one are both
+//    within 3 2^-24 sum |d_k p_k| <= 1.5 2^-24 (a + |p|^2) of the exact dot;
+//  * cs > 2^-18 rs: |p|^2 computed the reference's way exceeds r^2 (fused and
+//    reference sums within 2^-22 relative of |p|^2);
+//  * x < 75 a and cs + rs < 2^20 a (|p| < 1024 |d|): b < 150 a with the dot's
+//    error below 2^-12 a.
+// tests/test_oracle.py::test_behind_is_exact checks it against the reference's
+// own float test on adversarial rays.  RTG_BEHIND=0 (A/B builds) turns it off.
+#ifndef RTG_BEHIND
+#define RTG_BEHIND 1
+#endif
+RTG_HD bool behind(float a, float x, float cs, float rs) {
+  const float pp = cs + rs;
+  return RTG_BEHIND && x > 0x1p-20f * (a + pp) && cs > 0x1p-18f * rs && x < 75.f * a &&
+         pp < 0x1p20f * a;
+}
+// pass1_rad's screen and `behind` in one: false when sphere (c, rs) can have
+// no accepted root.
+RTG_HD bool screen_ahead(const RayQ& q, V3 c, float rs) {
+  const V3 p = vsub(q.o, c);
+  const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+  const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rs)));
+  const float v = fmaf(x, x, fmaf(-q.ap, cs, 0x1p-100f));
+  return !(v < 0.f) && !behind(0.5f * q.den, x, cs, rs);
 }
 
 // Screen radius^2 of pass1_rad, computed once per sphere on the host:
@@ -1374,24 +1423,32 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
       const V3 p = vsub(q.o, c);
       const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
       const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-      const float v = fmaf(xd, xd, fmaf(-q.ap, p2 - g[3], 0x1p-100f));  // pass1_rad
-      if (active && !beyond(p2, g[5], reachD) && !(v < 0.f)) leaf((unsigned)~x, c, g[4]);
+      const float cs = p2 - g[3];
+      const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
+      if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
+          !behind(0.5f * q.den, xd, cs, g[3]))
+        leaf((unsigned)~x, c, g[4]);
     }
   }
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
 }
 
+// (minT0, best0): a candidate already known (an accepted root of sphere
+// best0, or 1000 / -1): the answer is the lexicographic minimum of (t, i)
+// over every accepted root below 1000, so starting from any real candidate
+// gives the same answer with a shorter reach (closest_seeded).
 template <class Scene>
-RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
-  float minT = 1000.f;
-  int best = -1;
+RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 = 1000.f,
+                       int best0 = -1, bool active = true) {
+  float minT = minT0;
+  int best = best0;
   const float dn = norm_up(q.den * 0.5f);
   const BoxQ b = make_boxq(q);
   BvhStack st(sc.bvh_stack());
   unsigned nd = 0;  // the root
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
-    const int nx = bvh_ray_node(sc, q, b, nd, true, minT, minT * dn, st,
+    const int nx = bvh_ray_node(sc, q, b, nd, active, minT, minT * dn, st,
                                 [&](unsigned i, V3 ce, float r2) {
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
@@ -1515,7 +1572,7 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
   bool blk = false;
   auto step = [&](const ListRec& r) {
     sc.count(kUCapIter, 1);
-    if (!blk && !(pass1_rad(q, r.c, r.rs) < 0.f)) {
+    if (!blk && screen_ahead(q, r.c, r.rs)) {
       sc.count(kUShdExact, 1);
       bool res;
       const float t = ray_sphere(q, r.c, r.r2, res);
@@ -1561,7 +1618,7 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
     const int j = r.idx;
     if (j == h) return;
     sc.count(kUOvIter, 1);
-    if (!(pass1_rad(q, r.c, r.rs) < 0.f)) {
+    if (screen_ahead(q, r.c, r.rs)) {
       sc.count(kUEnterExact, 1);
       bool rj;
       const float t = ray_sphere(q, r.c, r.r2, rj);
@@ -1576,6 +1633,87 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
   }
   tOut = minT;
   return best;
+}
+
+// Closest hit of rays that start in sphere h's origin ball B''_h (every
+// active lane: a refraction child leaving h from its hit point P, P in h's
+// guard ball; or a reflection child from P + 0.01 rd), over h's neighbour
+// list (neighbour_lists, rtg_scene_pack.h): its records come in increasing
+// order of a certified lower bound delta on any accepted root's hit distance
+// t |d| from B''_h, so once a lane's best root has minT |d| < delta of the
+// next record (|d| rounded up, the product's rounding covered by the host's
+// delta (1 - 2^-20), rounded down), no later sphere can reach minT and the
+// lane's lexicographic minimum of (t, index) is the answer.  The list ends
+// with a terminator whose delta bounds every sphere left out (+inf when none
+// is); lanes it does not certify take the BVH from their best (closest_bvh,
+// certified lanes inactive).
+template <class Scene>
+RTG_HD int closest_near(const Scene& sc, const RayQ& q, int h, float& tOut) {
+  float minT = 1000.f;
+  int best = -1;
+  const float dn = norm_up(q.den * 0.5f);
+  unsigned k0, k1;
+  sc.nbr_range((unsigned)h, k0, k1);
+  bool cert = false;
+  auto step = [&](const ListRec& r) {
+    if (cert) return;
+    if (minT * dn < r.cr) {  // r.cr: the record's delta (1 - 2^-20), rounded down
+      cert = true;
+      return;
+    }
+    sc.count(kUNbrIter, 1);
+    if (screen_ahead(q, r.c, r.rs)) {
+      sc.count(kUBvhExact, 1);
+      bool rj;
+      const float t = ray_sphere(q, r.c, r.r2, rj);
+      const int j = r.idx;
+      if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
+    }
+  };
+  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
+    ListRec r0, r1;
+    sc.nbr_rec2(k, r0, r1);
+    step(r0);
+    if (sc.all(cert) || k + 1 >= k1) break;
+    step(r1);
+    if (sc.all(cert)) break;
+  }
+  tOut = minT;
+  if (sc.all(cert)) return best;
+  sc.count(kCntFullQ, 1);
+  return closest_bvh(sc, q, tOut, minT, best, !cert);
+}
+
+// Closest hit of rays that leave sphere h (every active lane: its hit point
+// P on h is the origin; refraction children that exit h, and (RTG_SEED_EXIT
+// >= 2) reflection children): the spheres that overlap h (h's overlap list)
+// are the likeliest first hits (P usually lies inside some of them in a dense
+// cluster), so their lexicographic minimum of (t, index) seeds the BVH query,
+// whose reach then starts at that t.  Any seed gives the same answer
+// (closest_bvh), so the list needs no geometric condition.
+template <class Scene>
+RTG_HD int closest_seeded(const Scene& sc, const RayQ& q, int h, float& tOut) {
+  float minT = 1000.f;
+  int best = -1;
+  unsigned k0, k1;
+  sc.ov_range((unsigned)h, k0, k1);
+  auto step = [&](const ListRec& r) {
+    sc.count(kUOvIter, 1);
+    if (screen_ahead(q, r.c, r.rs)) {
+      sc.count(kUBvhExact, 1);
+      bool rj;
+      const float t = ray_sphere(q, r.c, r.r2, rj);
+      const int j = r.idx;
+      if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
+    }
+  };
+  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
+    ListRec r0, r1;
+    sc.ov_rec2(k, r0, r1);
+    step(r0);
+    if (k + 1 < k1) step(r1);
+  }
+  return closest_bvh(sc, q, tOut, minT, best);
 }
 
 // primary_container (raytracer.h:245-270) for refraction test points of hits
@@ -1705,7 +1843,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
     sc.count(kUShdIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
-    if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
+    if (!blk && screen_ahead(q, c, rs)) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUShdExact, 1);
       bool res;
@@ -1856,7 +1994,7 @@ RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float
     sc.count(kUSelIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
-    if (!(pass1_rad(q, c, rs) < 0.f)) {
+    if (screen_ahead(q, c, rs)) {
       sc.count(kCntFullCand, 1);
       sc.count(kUSelExact, 1);
       bool res;

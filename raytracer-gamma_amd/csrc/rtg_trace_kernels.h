@@ -190,6 +190,8 @@ struct DevScene {
   int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
   cfloat_p capRec, ovRec;  // sphere lists of BVH scenes (sphere_lists) or null
   cuint_p capOff, ovOff;
+  cfloat_p nbrRec;  // neighbour lists of BVH scenes (neighbour_lists) or null
+  cuint_p nbrOff;
   unsigned n, m;
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
@@ -292,6 +294,20 @@ struct DevScene {
   }
   __device__ __forceinline__ void ov_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
+  }
+  // Neighbour lists (neighbour_lists, rtg_scene_pack.h): h's records are
+  // nbrOff[h] .. nbrOff[h + 1] (the last one h's terminator).
+  __device__ __forceinline__ bool has_nbr() const {
+    if constexpr (kBvh) return nbrOff != nullptr;
+    else return false;
+  }
+  __device__ __forceinline__ void nbr_range(unsigned h, unsigned& k0, unsigned& k1) const {
+    const cuint_p o = uidx(nbrOff, h);
+    k0 = o[0];
+    k1 = o[1];
+  }
+  __device__ __forceinline__ void nbr_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
+    list_rec2(nbrRec, k, r0, r1);
   }
   __device__ __forceinline__ V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
                                         float& rf) const {
@@ -514,6 +530,8 @@ struct KernelArgs {
   const unsigned* capOff;
   const float* ovRec;
   const unsigned* ovOff;
+  const float* nbrRec;    // neighbour lists (PackedScene::nbr*) or null
+  const unsigned* nbrOff;
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
@@ -646,6 +664,8 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.capOff = (cuint_p)a.capOff;
   sc.ovRec = (cfloat_p)a.ovRec;
   sc.ovOff = (cuint_p)a.ovOff;
+  sc.nbrRec = (cfloat_p)a.nbrRec;
+  sc.nbrOff = (cuint_p)a.nbrOff;
   // BVH scenes: 64 stack entries per wave after the frames and scene tables
   // (the launcher adds them to the LDS size).
   sc.bvhStk = reinterpret_cast<int*>(sceneLds + (kLds ? (a.n + 1) * 2 + a.n4 : 0)) +

@@ -64,6 +64,16 @@ struct HostScene {
   void ov_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
   }
+  const float* nbrRec = nullptr;
+  const unsigned* nbrOff = nullptr;
+  bool has_nbr() const { return nbrOff != nullptr; }
+  void nbr_range(unsigned h, unsigned& k0, unsigned& k1) const {
+    k0 = nbrOff[h];
+    k1 = nbrOff[h + 1];
+  }
+  void nbr_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
+    list_rec2(nbrRec, k, r0, r1);
+  }
   rtg::V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
     return list_rec(capRec, k, rs, r2, cr, idx, rf);
   }
@@ -172,6 +182,7 @@ struct HostScene {
 int g_variant = 0;
 bool g_useBvh = true;
 bool g_useLists = true;  // the sphere lists of BVH scenes (coherent-wave queries)
+bool g_useNbr = true;    // the neighbour lists of BVH scenes (closest_near)
 double g_boundM = 0.0;          // hostsim_bvh_bound_check: box margin probe (0: 2^-8)
 
 template <int S>
@@ -249,6 +260,7 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
 extern "C" void hostsim_use_lists(int on) { g_useLists = on != 0; }
+extern "C" void hostsim_use_nbr(int on) { g_useNbr = on != 0; }
 extern "C" void hostsim_bound_margin(double m) { g_boundM = m; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
 // the renders since the last reset (diagnostic; single-lane semantics, so the
@@ -283,6 +295,10 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
       sc.capOff = ps.capOff.data();
       sc.ovRec = ps.ovRec.data();
       sc.ovOff = ps.ovOff.data();
+      if (!ps.nbrOff.empty() && g_useNbr) {
+        sc.nbrRec = ps.nbrRec.data();
+        sc.nbrOff = ps.nbrOff.data();
+      }
     }
   }
   for (unsigned k = 0; k < nrows; ++k) {
@@ -828,4 +844,63 @@ extern "C" void hostsim_list_records(const rtg_sphere* spheres, unsigned n,
   if (ps.capOff.empty()) return;
   out[0] = ps.capRec.size() / rtg::kListWords - 1;  // without the padding record
   out[1] = ps.ovRec.size() / rtg::kListWords - 1;
+}
+
+// `behind` (rtg_trace.h) never rejects a sphere the reference's root test
+// accepts: adversarial rays from just outside a sphere, pointing away from
+// it or grazing it, at scales 1e-3 .. 1e3, unit and unnormalised directions,
+// against ray_sphere (raytracer.h:81-141's float operations).  Returns the
+// violations; *rejected counts the spheres behind() rejected, *loose the
+// accepted roots a margin-free version (x > 0, |p|^2 - r^2 > 0) would drop.
+extern "C" long hostsim_behind_check(long trials, unsigned long long seed, long* rejected,
+                                     long* loose) {
+  unsigned long long st = seed;
+  auto u01 = [&st]() {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    return (double)(st >> 11) * 0x1p-53;
+  };
+  long bad = 0;
+  *rejected = 0;
+  *loose = 0;
+  for (long k = 0; k < trials; ++k) {
+    const double scale = pow(10.0, -3.0 + 6.0 * u01());
+    const double r = scale * (0.05 + u01());
+    rtg::V3 c = rtg::v3((float)(scale * (u01() * 20 - 10)), (float)(scale * (u01() * 20 - 10)),
+                        (float)(scale * (u01() * 20 - 10)));
+    // a random unit normal n; the origin at distance r (1 + e) along n
+    double nx = u01() * 2 - 1, ny = u01() * 2 - 1, nz = u01() * 2 - 1;
+    const double nl = sqrt(nx * nx + ny * ny + nz * nz) + 1e-300;
+    nx /= nl; ny /= nl; nz /= nl;
+    const int kind = (int)(u01() * 4);
+    const double e = kind == 0 ? pow(10.0, -9.0 + 8.0 * u01()) : kind == 1 ? u01() * 3.0
+                   : pow(10.0, -7.0 + 7.0 * u01());
+    const float rf = (float)r;
+    rtg::V3 o = rtg::v3((float)(c.x + r * (1 + e) * nx), (float)(c.y + r * (1 + e) * ny),
+                        (float)(c.z + r * (1 + e) * nz));
+    // direction: away from the sphere with a tangential part (grazing when small)
+    double tx = u01() * 2 - 1, ty = u01() * 2 - 1, tz = u01() * 2 - 1;
+    const double tn = tx * nx + ty * ny + tz * nz;
+    tx -= tn * nx; ty -= tn * ny; tz -= tn * nz;
+    const double away = kind == 3 ? pow(10.0, -8.0 + 8.0 * u01()) : u01();
+    double dx = nx * away + tx, dy = ny * away + ty, dz = nz * away + tz;
+    const double dl = sqrt(dx * dx + dy * dy + dz * dz) + 1e-300;
+    const double dscale = (u01() < 0.5) ? 1.0 : pow(10.0, -1.5 + 3.0 * u01());
+    rtg::V3 d = rtg::v3((float)(dx / dl * dscale), (float)(dy / dl * dscale),
+                        (float)(dz / dl * dscale));
+    const rtg::RayQ q = rtg::make_query(o, d);
+    const float r2 = rf * rf;
+    const float rs = rtg::screen_r2(r2);
+    const rtg::V3 p = rtg::vsub(q.o, c);
+    const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+    const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rs)));
+    bool res;
+    (void)rtg::ray_sphere(q, c, r2, res);
+    if (rtg::behind(0.5f * q.den, x, cs, rs)) {
+      ++*rejected;
+      if (res) ++bad;
+    } else if (res && x > 0.f && fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -r2))) > 0.f) {
+      ++*loose;  // outside and receding by the fused terms, yet a root is accepted
+    }
+  }
+  return bad;
 }

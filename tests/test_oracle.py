@@ -453,6 +453,24 @@ def test_bvh_large_coordinates(hostsim, oracle):
         assert bits_equal(got, want), (scale, first_mismatch(got, want))
 
 
+def test_behind_is_exact(hostsim):
+    """`behind` (rtg_trace.h: the sphere lies wholly behind the ray's origin,
+    proven from the pass-1 screen's fused terms) never drops a sphere the
+    reference's own float root test accepts, over 4M adversarial rays from
+    just outside a sphere (gaps 1e-9 r .. 3 r), pointing away from it or
+    grazing it, at scales 1e-3 .. 1e3 with unit and unnormalised directions;
+    and the margins matter: dropping them (x > 0, |p|^2 - r^2 > 0 only)
+    would drop accepted roots."""
+    f = hostsim.hostsim_behind_check
+    f.restype = ctypes.c_long
+    rej, loose = ctypes.c_long(0), ctypes.c_long(0)
+    bad = f(ctypes.c_long(4_000_000), ctypes.c_ulonglong(2024), ctypes.byref(rej),
+            ctypes.byref(loose))
+    assert bad == 0, bad
+    assert rej.value > 1_000_000, rej.value
+    assert loose.value > 0, loose.value
+
+
 def test_cone_masks_are_conservative(hostsim):
     """Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): a sphere left
     out of mask (h, cell(U)) is never hit, by the reference's own root test,

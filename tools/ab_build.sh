@@ -12,7 +12,7 @@ WT=/tmp/rtg_ab_$NAME
 rm -rf "$WT"
 git -C "$ROOT" worktree prune
 git -C "$ROOT" worktree add --detach "$WT" "$REV" > /dev/null
-make -s -j"${JOBS:-8}" -C "$WT/raytracer-gamma_amd" ARCH=gfx950 EXTRA="${EXTRA:-}" librtg.so
+make -s -j"${JOBS:-8}" -C "$WT/raytracer-gamma_amd" ARCH=gfx950 AB="${AB:-0}" EXTRA="${EXTRA:-}" librtg.so
 mkdir -p "$ROOT/ab"
 cp "$WT/raytracer-gamma_amd/librtg.so" "$ROOT/ab/librtg_$NAME.so"
 git -C "$ROOT" worktree remove --force "$WT"
