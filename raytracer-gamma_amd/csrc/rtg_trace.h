@@ -1171,7 +1171,10 @@ RTG_HD float pass1_rad(const RayQ& q, V3 c, float rs) {
 //  * x < 75 a and cs + rs < 2^20 a (|p| < 1024 |d|): b < 150 a with the dot's
 //    error below 2^-12 a.
 // tests/test_oracle.py::test_behind_is_exact checks it against the reference's
-// own float test on adversarial rays.  RTG_BEHIND=0 (A/B builds) turns it off.
+// own float test on adversarial rays.  Used by the BVH scenes' queries (BVH
+// leaves, sphere lists): C5 138.8-138.9 vs 139.3-139.4 ms without; the
+// masked scenes' fused loops leave it out (C3 1.485-1.496 ms without it,
+// 1.508-1.532 with).  RTG_BEHIND=0 (A/B builds) turns it off.
 #ifndef RTG_BEHIND
 #define RTG_BEHIND 1
 #endif
@@ -1843,7 +1846,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
     sc.count(kUShdIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
-    if (!blk && screen_ahead(q, c, rs)) {
+    if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUShdExact, 1);
       bool res;
@@ -1994,7 +1997,7 @@ RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float
     sc.count(kUSelIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
-    if (screen_ahead(q, c, rs)) {
+    if (!(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntFullCand, 1);
       sc.count(kUSelExact, 1);
       bool res;
