@@ -148,10 +148,11 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
   return sel;
 }
 
-// A block takes kCullGroups = 4 x 256 consecutive groups (one per lane per
-// round) and appends its live ones with one atomic per run: the atomics on
-// the counters serialise in L2, so one per wave cost ~70 us on C3.
-constexpr unsigned kCullRounds = 4;
+// A block takes R x 256 consecutive groups (one per lane per round) and
+// appends its live ones with one atomic per run: the atomics on the counters
+// serialise in L2, so one per wave cost ~70 us on C3.  R (the launch picks
+// 1, 2 or 4) keeps at least ~4 blocks per CU: with R = 4 a C2 frame's pass
+// had 290 blocks (about one wave per SIMD) and took 24 us, latency-bound.
 // Each listed group's sphere mask goes to groupSel at the same list index:
 // the trace kernel takes it as the wave's primary-ray subset (one scalar
 // load) instead of recomputing the cull.
@@ -174,6 +175,7 @@ constexpr unsigned kCullRounds = 4;
 //    sphere mask: >= a.lptMin spheres first.
 // Run 0 fills the list's first half from the front, run 1 from its back,
 // runs 2 and 3 the second half likewise.
+template <unsigned kCullRounds>
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
                                                           unsigned long long* groupSel,
@@ -997,10 +999,21 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // previous launch's trace kernel (KernelArgs::zeroCount / zeroStat).
   if (slot) {
     const hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(
-        cull_groups_kernel,
-        dim3((unsigned)((cullGroups + 256 * kCullRounds - 1) / (256 * kCullRounds))), dim3(256),
-        0, st, a, cullGroups, slot->list, slot->sel, const_cast<unsigned*>(a.groupCount));
+    const size_t per4 = (size_t)256 * 4, minBlocks = (size_t)ctx->numCU * 4;
+    const unsigned rounds = cullGroups >= per4 * minBlocks       ? 4u
+                            : cullGroups >= per4 / 2 * minBlocks ? 2u
+                                                                 : 1u;
+    const dim3 cgrid((unsigned)((cullGroups + 256 * rounds - 1) / (256 * rounds)));
+    unsigned* cnt = const_cast<unsigned*>(a.groupCount);
+    if (rounds == 4)
+      hipLaunchKernelGGL(cull_groups_kernel<4>, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
+                         slot->sel, cnt);
+    else if (rounds == 2)
+      hipLaunchKernelGGL(cull_groups_kernel<2>, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
+                         slot->sel, cnt);
+    else
+      hipLaunchKernelGGL(cull_groups_kernel<1>, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
+                         slot->sel, cnt);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
       hipLaunchKernelGGL(fn, grid, dim3(threads), lds, st, a);

@@ -148,6 +148,10 @@ inline void prim_consts(const rtg_sphere& s, float* out) {
 // light L (capsule_keep; *tOut = its centre's position along c_h -> L, 0..1),
 // and sphere j can contain a refraction test point of h / be hit by a ray that
 // entered h before it leaves B_h (overlap_keep).  See shadow_masks.
+// Test hook (tests/hostsim only): a positive value moves capsule_keep's
+// back plane forward by that fraction of g, so the check can show that the
+// plane's position matters.
+inline double g_capsuleBackSlack = 0.0;
 inline bool capsule_keep(const rtg_sphere* spheres, unsigned h, unsigned i, const double L[3],
                          double* tOut = nullptr) {
   const rtg_sphere& sh = spheres[h];
@@ -168,7 +172,18 @@ inline bool capsule_keep(const rtg_sphere* spheres, unsigned h, unsigned i, cons
   dch = sqrt(dch);
   t = ab2 > 0.0 ? t / ab2 : 0.0;
   t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
-  if (tOut) *tOut = (i == h) ? -1.0 : t;
+  if (tOut) {
+    // The capsule list's order key (sphere_lists): h itself first, then the
+    // spheres whose extent along c_h -> L reaches back to the segment's start
+    // (the likeliest blockers of a shadow ray from the hit point: P lies
+    // inside or just behind them), largest first, then the others by where
+    // their extent starts.  Only the order of the walk depends on it.
+    double traw = 0.0;
+    for (int k = 0; k < 3; ++k) traw += (C[k] - A[k]) * ab[k];
+    traw = ab2 > 0.0 ? traw / ab2 : 0.0;
+    const double start = traw - ri / (lh > 0.0 ? lh : 1.0);
+    *tOut = (i == h) ? -1e300 : start < 0.0 ? -ri : start;
+  }
   if (i == h) return true;
   double d2 = 0.0;
   for (int k = 0; k < 3; ++k) {
@@ -177,7 +192,24 @@ inline bool capsule_keep(const rtg_sphere* spheres, unsigned h, unsigned i, cons
   }
   const double mu = 0x1p-8 * (dch + g + ri) + 0x1p-16 * (lh + g);
   const double reach = (g + ri + mu) * (1.0 + 1e-9);
-  return !(sqrt(d2) > reach);
+  if (sqrt(d2) > reach) return false;
+  // The kernel casts a shadow ray only from a point P with incidence > 0
+  // (matte_light): N.dir > 0 computed, so (P - c_h).(L - P) > -2^-20 |P -
+  // c_h| |L - P| exactly, whence (P - c_h).u >= -2^-19 g with u the unit
+  // vector c_h -> L (|L - P| <= 2 |L - c_h| for a light outside the guard
+  // ball).  Every point of the segment P -> L then lies in that half-space,
+  // and so does every blocking root's exact point, which is within r_i + mu
+  // of c_i: a sphere whose grown ball lies wholly behind the plane
+  // (c_i - c_h).u + r_i + mu < -(2^-16 g + 2^-20 |L - c_h|) blocks no
+  // shadow ray of h.
+  if (lh > 2.0 * g) {
+    double proj = 0.0;
+    for (int k = 0; k < 3; ++k) proj += (C[k] - A[k]) * ab[k];
+    proj /= lh;
+    if (proj + (ri + mu) * (1.0 + 1e-9) < -(0x1p-16 * g + 0x1p-20 * lh) + g_capsuleBackSlack * g)
+      return false;
+  }
+  return true;
 }
 inline bool overlap_keep(const rtg_sphere* spheres, unsigned h, unsigned j) {
   if (j == h) return true;
@@ -239,8 +271,10 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
 // masks' sets as lists of kListWords-word records, for the coherent-wave
 // queries of rtg_trace.h (blocked_cap, closest_enter_list, container_list):
 //  * capsule lists, one per (light l, sphere h): the spheres of shadow mask
-//    (l, h) (capsule_keep), nearest first along c_h -> L_l (h itself first),
-//    records {x, y, z, screen r^2 (screen_r2), r^2, 0, 0, 0};
+//    (l, h) (capsule_keep) in the order of capsule_keep's key (h itself
+//    first, then the spheres that reach back to the segment's start, largest
+//    first: the likeliest blockers), records {x, y, z, screen r^2
+//    (screen_r2), r^2, 0, 0, 0};
 //  * overlap lists, one per sphere h: the spheres of overlap mask h
 //    (overlap_keep) in index order, records {x, y, z, screen r^2, r^2,
 //    (r + 1e-6f)^2, index, refractive index}.
@@ -283,8 +317,8 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
                                  s.material.refractiveIndex};
     v.insert(v.end(), w, w + kListWords);
   };
-  // capsule lists: per (l, h) the kept spheres sorted by position along the
-  // capsule; the (l, h) pairs are independent, so they are built in parallel
+  // capsule lists: per (l, h) the kept spheres sorted by capsule_keep's key;
+  // the (l, h) pairs are independent, so they are built in parallel
   std::vector<std::vector<unsigned>> lists((size_t)m * n);
   auto work = [&](unsigned lo, unsigned hi) {
     std::vector<std::pair<double, unsigned>> tmp;

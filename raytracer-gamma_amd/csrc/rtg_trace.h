@@ -1560,7 +1560,7 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
 
 // Shadow ray from a hit point P of sphere h (guard test passed) to light l:
 // only the spheres of h's capsule list can block it (shadow_masks' argument),
-// and the list is ordered nearest first, so blocked lanes stop early; the
+// and the list holds the likeliest blockers first, so blocked lanes stop early; the
 // wave leaves once every lane is blocked.  Same answer as blocked_bvh: any
 // blocker.
 // The list loops below take records in pairs, k and k + 1, from one 64-byte

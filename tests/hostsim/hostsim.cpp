@@ -261,6 +261,7 @@ extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
 extern "C" void hostsim_use_lists(int on) { g_useLists = on != 0; }
 extern "C" void hostsim_use_nbr(int on) { g_useNbr = on != 0; }
+extern "C" void hostsim_capsule_back_slack(double s) { rtg::g_capsuleBackSlack = s; }
 extern "C" void hostsim_bound_margin(double m) { g_boundM = m; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
 // the renders since the last reset (diagnostic; single-lane semantics, so the
@@ -454,6 +455,31 @@ extern "C" long hostsim_shadow_mask_check(long scenes, unsigned n, long points,
       lg[l].pos.y = (float)((10 + 70 * u01()) * scale);
       lg[l].pos.z = (float)((u01() - 0.5) * 130 * scale);
     }
+    // a quarter of the spheres: just behind sphere 0's plane facing light 0
+    // (wholly on the far side of c_0, within the capsule's radius), which only
+    // rays from points with incidence <= 0 could cross
+    for (unsigned i = n / 4; i < n / 2; ++i) {
+      const rtg_sphere& h = sph[0];
+      const double A[3] = {h.pos.x, h.pos.y, h.pos.z};
+      const double L[3] = {lg[0].pos.x, lg[0].pos.y, lg[0].pos.z};
+      double ab[3], ab2 = 0.0;
+      for (int k = 0; k < 3; ++k) { ab[k] = L[k] - A[k]; ab2 += ab[k] * ab[k]; }
+      const double lh = sqrt(ab2);
+      double v[3] = {u01() - 0.5, u01() - 0.5, u01() - 0.5};
+      const double pr = (v[0] * ab[0] + v[1] * ab[1] + v[2] * ab[2]) / ab2;
+      for (int k = 0; k < 3; ++k) v[k] -= pr * ab[k];
+      const double vl = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      const double ri = sph[i].radius;
+      const double g = rtg::guard_radius(h);
+      // centre this far behind: the sphere's front just behind or just ahead
+      // of the plane
+      const double back = ri * (1.0 + (u01() < 0.5 ? -1.0 : 1.0) * pow(10.0, -6.0 + 4.0 * u01()));
+      const double lat = (g + ri) * u01();
+      for (int k = 0; k < 3; ++k) {
+        const double c = A[k] - back * ab[k] / lh + lat * v[k] / vl;
+        (k == 0 ? sph[i].pos.x : k == 1 ? sph[i].pos.y : sph[i].pos.z) = (float)c;
+      }
+    }
     // half of the spheres: just outside (or on) the capsule of (light 0, sphere 0)
     for (unsigned i = n / 2; i < n; ++i) {
       const rtg_sphere& h = sph[0];
@@ -497,6 +523,21 @@ extern "C" long hostsim_shadow_mask_check(long scenes, unsigned n, long points,
               const double spread = pow(10.0, -3.0 * u01());
               ux = cx / cl + spread * ux; uy = cy / cl + spread * uy; uz = cz / cl + spread * uz;
             }
+            if (k % 4 == 3) {  // on h's rim facing light l, toward sphere i (grazing rays)
+              const double lx = (double)lg[l].pos.x - sh.pos.x, ly = (double)lg[l].pos.y - sh.pos.y,
+                           lz = (double)lg[l].pos.z - sh.pos.z;
+              const double ll = sqrt(lx * lx + ly * ly + lz * lz) + 1e-300;
+              double cx = (double)sph[i].pos.x - sh.pos.x, cy = (double)sph[i].pos.y - sh.pos.y,
+                     cz = (double)sph[i].pos.z - sh.pos.z;
+              const double pr = (cx * lx + cy * ly + cz * lz) / (ll * ll);
+              cx -= pr * lx; cy -= pr * ly; cz -= pr * lz;
+              const double cl = sqrt(cx * cx + cy * cy + cz * cz) + 1e-300;
+              const double up = pow(10.0, -5.0 + 4.0 * u01());
+              const double side = 1e-3 * (u01() - 0.5);
+              ux = cx / cl + up * lx / ll + side * (u01() - 0.5);
+              uy = cy / cl + up * ly / ll + side * (u01() - 0.5);
+              uz = cz / cl + up * lz / ll + side * (u01() - 0.5);
+            }
             const double ul = sqrt(ux * ux + uy * uy + uz * uz);
             const double rad = (k % 6 == 0) ? g * u01()
                                              : fabs((double)sh.radius) * (1.0 + (u01() - 0.7) * 2e-3);
@@ -509,6 +550,10 @@ extern "C" long hostsim_shadow_mask_check(long scenes, unsigned n, long points,
             const rtg::V3 dist = rtg::vsub(Lp, P);
             const float gap = rtg::vdot(dist, dist);
             const rtg::V3 D = rtg::vsmul(1.f / sqrtf(gap), dist);
+            // the kernel casts a shadow ray only when the incidence is > 0
+            // (matte_light, raytracer.h:337-349)
+            const rtg::V3 N = rtg::vnorm(e);
+            if (!(rtg::vdot(N, D) > 0.f)) continue;
             const rtg::RayQ q = rtg::make_query(P, D);
             ++cnt;
             bool res;

@@ -255,14 +255,25 @@ def test_shadow_masks_are_conservative(hostsim):
     blocks a shadow ray from a hit point inside the guard ball to the light,
     by the reference's own test (raytracer.h:272-309), over random scenes at
     scales 1e-2..1e2 with half of the spheres placed just outside the capsule
-    reach (relative gaps 1e-4..3e-2)."""
+    reach (relative gaps 1e-4..3e-2) and a quarter just behind the hit
+    sphere's plane facing the light (which the masks drop: a shadow ray is
+    cast only from points with incidence > 0); the hit points include
+    grazing ones.  Moving that plane forward by 2^-5 g (past the margin mu)
+    finds blockers."""
     f = hostsim.hostsim_shadow_mask_check
     f.restype = ctypes.c_long
+    hostsim.hostsim_capsule_back_slack.argtypes = [ctypes.c_double]
     tested = ctypes.c_long(0)
-    bad = f(ctypes.c_long(400), 12, ctypes.c_long(60), ctypes.c_ulonglong(99),
+    bad = f(ctypes.c_long(600), 12, ctypes.c_long(60), ctypes.c_ulonglong(99),
             ctypes.byref(tested))
     assert bad == 0, bad
     assert tested.value > 1_000_000, tested.value
+    try:
+        hostsim.hostsim_capsule_back_slack(2.0 ** -5)
+        assert f(ctypes.c_long(300), 12, ctypes.c_long(60), ctypes.c_ulonglong(98),
+                 ctypes.byref(tested)) > 0  # the check has teeth
+    finally:
+        hostsim.hostsim_capsule_back_slack(0.0)
 
 
 @pytest.mark.parametrize("name", ["c2", "c3", "c4"])
