@@ -258,6 +258,28 @@ struct FrameC {
                   // inside: the reflection child starts inside the origin sphere)
 };
 struct FrameR { V3 ro, rd, rI; };
+RTG_HD void frame_r_store(FrameR& dst, const FrameR& v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float* d = &dst.ro.x;
+  const float* s = &v.ro.x;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) __builtin_nontemporal_store(s[k], d + k);
+#else
+  dst = v;
+#endif
+}
+RTG_HD FrameR frame_r_load(const FrameR& src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  FrameR v;
+  float* d = &v.ro.x;
+  const float* s = &src.ro.x;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) d[k] = __builtin_nontemporal_load(s + k);
+  return v;
+#else
+  return src;
+#endif
+}
 
 // Local (private-memory) storage of the colour part, used when the scene does
 // not provide per-lane LDS frames.
@@ -305,6 +327,11 @@ struct Frame {
 #ifndef RTG_SEED_EXIT
 #define RTG_SEED_EXIT 0
 #endif
+// A/B builds (RTG_SCRATCH_NT=1): the reflection child rays' scratch stores
+// and loads with the nontemporal cache policy (scratch traffic).
+#ifndef RTG_SCRATCH_NT
+#define RTG_SCRATCH_NT 0
+#endif
 struct RayQ {
   V3 o, d;
   float a4, den, y;
@@ -345,8 +372,31 @@ RTG_HD float quot(float x, const RayQ& q) {
   return r;
 }
 
+// No root of the reference's test can be accepted (raytracer.h:105-138)
+// when, in its own values b and cc, b > 0 and b < 16 a and either cc >= 0
+// (the origin outside and the centre behind it: radicand <= fl(b b), so
+// -b + root <= 2^-23 b (exact, Sterbenz) and u0 <= 2^-23 b / 2a < 1e-6), or
+// cc < 0 with -cc < 8e-6 b (the origin inside by a rounding, typically the
+// hit point on its own sphere: root <= (b + 2a |cc| / b)(1 + 2.0001 eps), so
+// u0 <= |cc| / b (1 + 3 eps) + 2.0001 eps b / a (1 + eps) < 8.96e-6 < 1e-5);
+// u1 < 0 in both cases.  Shadow rays test their own hit sphere first
+// (capsule lists, masks): its wave then skips the square root and the
+// quotients unless a lane grazes it.  tests/test_oracle.py::
+// test_no_root_is_exact checks it against the reference's test.
+#ifndef RTG_NOROOT  // 0 off, 1 shadow queries (default), 2 every BVH-scene query
+#define RTG_NOROOT 1
+#endif
+#ifndef RTG_NOROOT_K  // the inside bound (tests probe larger ones)
+#define RTG_NOROOT_K 8e-6f
+#endif
+RTG_HD bool no_root(const RayQ& q, float b, float cc) {
+  return b > 0.f && b < 4.f * q.a4 && (cc >= 0.f || -cc < RTG_NOROOT_K * b);
+}
+
 // Per-sphere ray test, raytracer.h:81-141.  Returns the smallest root in
-// (1e-5, 10000) or 10000 when none (`res` tells).
+// (1e-5, 10000) or 10000 when none (`res` tells).  kNone: lanes where
+// no_root holds skip the roots (same answer).
+template <bool kNone = false>
 RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   V3 disp = vsub(q.o, c);
   const float b = 2.0f * vdot(q.d, disp);
@@ -354,7 +404,7 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   const float radicand = (b * b) - (q.a4 * cc);
   float sm = 10000.f;
   res = false;
-  if (radicand >= 0.0f) {
+  if (radicand >= 0.0f && !(kNone && no_root(q, b, cc))) {
     const float root = rtg_sqrtf(radicand);
     const float u0 = quot(-b + root, q);
     const float u1 = quot(-b - root, q);
@@ -379,7 +429,7 @@ RTG_HD float quot_k(float x, const RayQ& q) {
   }
 }
 
-template <bool kFast>
+template <bool kFast, bool kNone = false>
 RTG_HD float ray_sphere_k(const RayQ& q, V3 c, float r2, bool& res) {
   V3 disp = vsub(q.o, c);
   const float b = 2.0f * vdot(q.d, disp);
@@ -387,7 +437,7 @@ RTG_HD float ray_sphere_k(const RayQ& q, V3 c, float r2, bool& res) {
   const float radicand = (b * b) - (q.a4 * cc);
   float sm = 10000.f;
   res = false;
-  if (radicand >= 0.0f) {
+  if (radicand >= 0.0f && !(kNone && no_root(q, b, cc))) {
     const float root = rtg_sqrtf(radicand);
     const float u0 = quot_k<kFast>(-b + root, q);
     const float u1 = quot_k<kFast>(-b - root, q);
@@ -973,6 +1023,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             r.ro = vadd(P, vsmul(0.01f, rd));
             r.rI = rc;
             if (RTG_FR0_REGS && lv == 0) fr0 = r;
+            else if (RTG_SCRATCH_NT) frame_r_store(fr[lv], r);
             else fr[lv] = r;
 #if RTG_SCRATCH_X2
             frx[lv] = r;
@@ -1024,7 +1075,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
 #if defined(__HIP_DEVICE_COMPILE__)
           if (RTG_FR0_REGS) asm volatile("" ::: "memory");  // no speculative scratch load
 #endif
-          r = fr[lv];
+          r = RTG_SCRATCH_NT ? frame_r_load(fr[lv]) : fr[lv];
         }
 #if RTG_SCRATCH_X2 && defined(__HIP_DEVICE_COMPILE__)
         {
@@ -1456,7 +1507,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere(q, ce, r2, res);
+      const float t = ray_sphere<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       if (res && (t < minT || (t == minT && (int)i < best))) {
         minT = t;
         best = (int)i;
@@ -1493,7 +1544,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere(q, ce, r2, res);
+      const float t = ray_sphere<(RTG_NOROOT >= 1)>(q, ce, r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
@@ -1578,7 +1629,7 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
     if (!blk && screen_ahead(q, r.c, r.rs)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere(q, r.c, r.r2, res);
+      const float t = ray_sphere<(RTG_NOROOT >= 1)>(q, r.c, r.r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
@@ -1850,7 +1901,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
       sc.count(kCntShadowCand, 1);
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere_k<kFast>(q, c, r2, res);
+      const float t = ray_sphere_k<kFast, (RTG_NOROOT >= 1)>(q, c, r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;

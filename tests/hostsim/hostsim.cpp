@@ -949,3 +949,56 @@ extern "C" long hostsim_behind_check(long trials, unsigned long long seed, long*
   }
   return bad;
 }
+
+// no_root (rtg_trace.h) never skips a root the reference accepts: rays from
+// on, just inside or just outside a sphere's surface (the shadow ray of a
+// hit point on its own sphere), leaving it at any angle down to grazing, at
+// scales 1e-3 .. 1e2 with unit and unnormalised directions.  Returns the
+// violations; *skipped counts the tests no_root skipped, *accepted the roots
+// the reference accepted (self-shadowing acne: the check has cases to miss).
+extern "C" long hostsim_no_root_check(long trials, unsigned long long seed, long* skipped,
+                                      long* accepted) {
+  unsigned long long st = seed;
+  auto u01 = [&st]() {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    return (double)(st >> 11) * 0x1p-53;
+  };
+  long bad = 0;
+  *skipped = 0;
+  *accepted = 0;
+  for (long k = 0; k < trials; ++k) {
+    const double scale = pow(10.0, -3.0 + 5.0 * u01());
+    const double r = scale * (0.05 + u01());
+    const rtg::V3 c = rtg::v3((float)(scale * (u01() * 20 - 10)), (float)(scale * (u01() * 20 - 10)),
+                              (float)(scale * (u01() * 20 - 10)));
+    double nx = u01() * 2 - 1, ny = u01() * 2 - 1, nz = u01() * 2 - 1;
+    const double nl = sqrt(nx * nx + ny * ny + nz * nz) + 1e-300;
+    nx /= nl; ny /= nl; nz /= nl;
+    const double e = (u01() - 0.5) * pow(10.0, -8.0 + 5.0 * u01());  // on / inside / outside
+    const rtg::V3 o = rtg::v3((float)(c.x + r * (1 + e) * nx), (float)(c.y + r * (1 + e) * ny),
+                              (float)(c.z + r * (1 + e) * nz));
+    double tx = u01() * 2 - 1, ty = u01() * 2 - 1, tz = u01() * 2 - 1;
+    const double tn = tx * nx + ty * ny + tz * nz;
+    tx -= tn * nx; ty -= tn * ny; tz -= tn * nz;
+    const double tl = sqrt(tx * tx + ty * ty + tz * tz) + 1e-300;
+    const double cosv = (u01() < 0.5) ? pow(10.0, -7.0 + 7.0 * u01()) : u01();  // to grazing
+    const double sinv = sqrt(1 - cosv * cosv);
+    const double dscale = (u01() < 0.5) ? 1.0 : pow(10.0, -1.0 + 2.0 * u01());
+    const rtg::V3 d = rtg::v3((float)((nx * cosv + tx / tl * sinv) * dscale),
+                              (float)((ny * cosv + ty / tl * sinv) * dscale),
+                              (float)((nz * cosv + tz / tl * sinv) * dscale));
+    const rtg::RayQ q = rtg::make_query(o, d);
+    const float r2 = (float)r * (float)r;
+    const rtg::V3 disp = rtg::vsub(q.o, c);
+    const float b = 2.0f * rtg::vdot(q.d, disp);
+    const float cc = rtg::vdot(disp, disp) - r2;
+    bool res;
+    (void)rtg::ray_sphere(q, c, r2, res);
+    if (res) ++*accepted;
+    if (rtg::no_root(q, b, cc)) {
+      ++*skipped;
+      if (res) ++bad;
+    }
+  }
+  return bad;
+}

@@ -482,6 +482,21 @@ def test_behind_is_exact(hostsim):
     assert loose.value > 0, loose.value
 
 
+def test_no_root_is_exact(hostsim):
+    """`no_root` (rtg_trace.h: the reference's own b and cc show that no root
+    can be accepted) never skips a root the reference's float test accepts,
+    over 4M rays from on / just inside / just outside a sphere's surface
+    leaving it at angles down to grazing (the shadow ray of a hit point
+    against its own sphere), scales 1e-3 .. 1e2, unit and unnormalised
+    directions; the set includes accepted self-hits (grazing acne)."""
+    f = hostsim.hostsim_no_root_check
+    f.restype = ctypes.c_long
+    sk, acc = ctypes.c_long(0), ctypes.c_long(0)
+    bad = f(ctypes.c_long(4_000_000), ctypes.c_ulonglong(77), ctypes.byref(sk), ctypes.byref(acc))
+    assert bad == 0, bad
+    assert sk.value > 1_000_000 and acc.value > 1000, (sk.value, acc.value)
+
+
 def test_cone_masks_are_conservative(hostsim):
     """Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): a sphere left
     out of mask (h, cell(U)) is never hit, by the reference's own root test,
