@@ -379,11 +379,14 @@ RTG_HD float quot(float x, const RayQ& q) {
 // cc < 0 with -cc < 8e-6 b (the origin inside by a rounding, typically the
 // hit point on its own sphere: root <= (b + 2a |cc| / b)(1 + 2.0001 eps), so
 // u0 <= |cc| / b (1 + 3 eps) + 2.0001 eps b / a (1 + eps) < 8.96e-6 < 1e-5);
-// u1 < 0 in both cases.  Shadow rays test their own hit sphere first
-// (capsule lists, masks): its wave then skips the square root and the
-// quotients unless a lane grazes it.  tests/test_oracle.py::
+// u1 < 0 in both cases.  Shadow rays test their own hit sphere (in their
+// mask): its wave then skips the square root and the quotients unless a
+// lane grazes it.  tests/test_oracle.py::
 // test_no_root_is_exact checks it against the reference's test.
-#ifndef RTG_NOROOT  // 0 off, 1 shadow queries (default), 2 every BVH-scene query
+// Default (1): the masked scenes' shadow queries (C3 -0.9 %, C4 -1 %); the
+// BVH scenes' (2) cost the BVH kernel two VGPRs past 80, one wave per SIMD
+// less: C5 145.5 vs 130.1 ms.
+#ifndef RTG_NOROOT  // 0 off, 1 masked-scene shadow queries, 2 also BVH-scene shadow queries
 #define RTG_NOROOT 1
 #endif
 #ifndef RTG_NOROOT_K  // the inside bound (tests probe larger ones)
@@ -1544,7 +1547,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere<(RTG_NOROOT >= 1)>(q, ce, r2, res);
+      const float t = ray_sphere<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
@@ -1629,7 +1632,7 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
     if (!blk && screen_ahead(q, r.c, r.rs)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere<(RTG_NOROOT >= 1)>(q, r.c, r.r2, res);
+      const float t = ray_sphere<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
