@@ -1454,6 +1454,20 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
                         bool shadowQ = false) {
   BvhRec r;
   sc.bvh_rec(nd, r);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_SALU)  // issue-cost probes (A/B builds)
+  {
+    unsigned pad;
+#pragma unroll
+    for (int k = 0; k < RTG_PAD_BVH_SALU; ++k) asm volatile("s_add_u32 %0, 7, 1" : "=s"(pad));
+  }
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_VALU)
+  {
+    float pad;
+#pragma unroll
+    for (int k = 0; k < RTG_PAD_BVH_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, 2.0" : "=v"(pad));
+  }
+#endif
   int pc[4];
   float pk[4];
 #pragma unroll
