@@ -1458,7 +1458,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
   {
     unsigned pad;
 #pragma unroll
-    for (int k = 0; k < RTG_PAD_BVH_SALU; ++k) asm volatile("s_add_u32 %0, 7, 1" : "=s"(pad));
+    for (int k = 0; k < RTG_PAD_BVH_SALU; ++k) asm volatile("s_mov_b32 %0, 7" : "=s"(pad));  // no SCC write
   }
 #endif
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_VALU)
