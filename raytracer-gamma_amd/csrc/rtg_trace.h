@@ -1423,6 +1423,31 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2,
       const unsigned kt = ka; ka = kb; kb = kt;
     }
   };
+#ifndef RTG_BVH_SORT  // experiment: 1 = nearest next, the others pushed in slot order
+#define RTG_BVH_SORT 0
+#endif
+  if (RTG_BVH_SORT == 1) {
+    // nearest to the front (three compares), the rest keep their slot order
+    cx(c0, k0, c1, k1);
+    cx(c1, k1, c2, k2);
+    cx(c2, k2, c3, k3);
+    // c3 now holds the nearest; push c0..c2 (farther), then return c3
+    int nx = 0;
+    auto put1 = [&](int c) {
+      if (c > 0) {
+        if (nx > 0) st.push(nx);
+        nx = c;
+      }
+    };
+    put1(c0);
+    put1(c1);
+    put1(c2);
+    if (c3 > 0) {
+      if (nx > 0) st.push(nx);
+      nx = c3;
+    }
+    return nx;
+  }
   cx(c0, k0, c1, k1);
   cx(c2, k2, c3, k3);
   cx(c0, k0, c2, k2);
