@@ -417,6 +417,40 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   return sm;
 }
 
+// The same test with selects in place of the divergent branches (for the
+// BVH scenes' leaf and list loops, whose waves are scalar-issue bound: each
+// divergent if costs an exec-mask save, a branch and a restore).  Lanes with
+// a negative radicand compute discarded roots; the square root's fallback
+// and the quotient's stay wave-uniform branches (RTG_SEL_EXACT=0: branches).
+#ifndef RTG_SEL_EXACT
+#define RTG_SEL_EXACT 0
+#endif
+RTG_HD float ray_sphere_sel(const RayQ& q, V3 c, float r2, bool& res) {
+  V3 disp = vsub(q.o, c);
+  const float b = 2.0f * vdot(q.d, disp);
+  const float cc = vdot(disp, disp) - r2;
+  const float radicand = (b * b) - (q.a4 * cc);
+  const bool ok = radicand >= 0.0f;
+  float root = sqrt_fast(radicand);  // (NaN for a negative radicand: not used)
+  if (any_lane(ok && !sqrt_fast_range(radicand))) {
+    no_speculate();
+    if (ok && !sqrt_fast_range(radicand)) root = sqrtf(radicand);
+  }
+  const float u0 = quot(-b + root, q);
+  const float u1 = quot(-b - root, q);
+  const bool a0 = ok && u0 > 1.0e-5f && u0 < 10000.f;
+  float sm = a0 ? u0 : 10000.f;
+  const bool a1 = ok && u1 > 1.0e-5f && u1 < sm;
+  sm = a1 ? u1 : sm;
+  res = a0 || a1;
+  return sm;
+}
+template <bool kNone = false>
+RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res) {
+  if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);
+  return ray_sphere<kNone>(q, c, r2, res);
+}
+
 // The same with the quotient path chosen for the whole wave (kFast: every
 // lane's denominator is in the Markstein range, all(q.fast)).
 template <bool kFast>
@@ -1549,7 +1583,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere<(RTG_NOROOT >= 2)>(q, ce, r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       if (res && (t < minT || (t == minT && (int)i < best))) {
         minT = t;
         best = (int)i;
@@ -1586,7 +1620,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere<(RTG_NOROOT >= 2)>(q, ce, r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
@@ -1671,7 +1705,7 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
     if (!blk && screen_ahead(q, r.c, r.rs)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;
@@ -1717,7 +1751,7 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
     if (screen_ahead(q, r.c, r.rs)) {
       sc.count(kUEnterExact, 1);
       bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj);
+      const float t = ray_sphere_leaf(q, r.c, r.r2, rj);
       if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
     }
   };
