@@ -1435,14 +1435,21 @@ struct BvhRec {
   float cr[4];
 };
 
-// Children of a node in front-to-back order for the wave: of the valid
-// (child, key) pairs, keys = a lane's box entry parameter (wave-uniform), the
-// nearest is returned (the next node: no stack round trip) and the others are
-// pushed farthest first.  Five compare-exchanges.  The keys are compared as
-// unsigned bit patterns: an entry parameter is max(..., 0) >= 0 and never NaN
-// (slab_pass), and for such floats the patterns order like the values (a -0
-// would sort last; the order only decides which node is visited first, never
-// an answer), so the compare-exchanges are scalar integer work.
+// Children of a node for the wave: of the valid (child, key) pairs, keys =
+// a lane's box entry parameter (wave-uniform), the nearest is returned (the
+// next node: no stack round trip) and the others are pushed in slot order.
+// Three compare-exchanges bubble the nearest to the end.  The keys are
+// compared as unsigned bit patterns: an entry parameter is max(..., 0) >= 0
+// and never NaN (slab_pass), and for such floats the patterns order like the
+// values (a -0 would sort last; the order only decides which node is visited
+// first, never an answer), so the compare-exchanges are scalar integer work.
+// The waves are scalar-issue bound (an extra scalar instruction per node
+// costs 2.4 times an extra vector one): a full
+// five-exchange sort visited 1 % fewer nodes and ran C5 4 % slower
+// (RTG_BVH_SORT=0, A/B builds).
+#ifndef RTG_BVH_SORT
+#define RTG_BVH_SORT 1
+#endif
 RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2, float f2,
                        int c3, float f3) {
   auto bits = [](float f) {
@@ -1457,36 +1464,17 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2,
       const unsigned kt = ka; ka = kb; kb = kt;
     }
   };
-#ifndef RTG_BVH_SORT  // experiment: 1 = nearest next, the others pushed in slot order
-#define RTG_BVH_SORT 0
-#endif
-  if (RTG_BVH_SORT == 1) {
-    // nearest to the front (three compares), the rest keep their slot order
+  if (RTG_BVH_SORT == 0) {  // full sort: the others pushed farthest first
+    cx(c0, k0, c1, k1);
+    cx(c2, k2, c3, k3);
+    cx(c0, k0, c2, k2);
+    cx(c1, k1, c3, k3);
+    cx(c1, k1, c2, k2);
+  } else {  // the nearest to c3 (an invalid child has child 0 and the largest key)
     cx(c0, k0, c1, k1);
     cx(c1, k1, c2, k2);
     cx(c2, k2, c3, k3);
-    // c3 now holds the nearest; push c0..c2 (farther), then return c3
-    int nx = 0;
-    auto put1 = [&](int c) {
-      if (c > 0) {
-        if (nx > 0) st.push(nx);
-        nx = c;
-      }
-    };
-    put1(c0);
-    put1(c1);
-    put1(c2);
-    if (c3 > 0) {
-      if (nx > 0) st.push(nx);
-      nx = c3;
-    }
-    return nx;
   }
-  cx(c0, k0, c1, k1);
-  cx(c2, k2, c3, k3);
-  cx(c0, k0, c2, k2);
-  cx(c1, k1, c3, k3);
-  cx(c1, k1, c2, k2);
   int nxt = 0;
   auto put = [&](int c) {
     if (c > 0) {
@@ -1529,10 +1517,15 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
 #endif
   int pc[4];
   float pk[4];
+  float keyMax;  // bit pattern 0xFFFFFFFF: an invalid child sorts last (push_sorted)
+  {
+    const unsigned u = 0xFFFFFFFFu;
+    memcpy(&keyMax, &u, 4);
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     pc[k] = 0;
-    pk[k] = 0.f;
+    pk[k] = keyMax;
     const int x = r.ch[k];
     if (x == 0) continue;  // wave-uniform
     sc.count(kUBvhSlot, 1);
