@@ -65,8 +65,11 @@ def test_edge_cases(R, golden):
         assert bits_equal(got, want), (c["name"], first_mismatch(got, want))
 
 
-@pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4"])
+@pytest.mark.parametrize("name", ["ref800", "c1", "c2", "c3", "c4", "c5"])
 def test_full_frames_md5_and_ppm(R, golden, tmp_path, name):
+    """Whole frames against the reference's: canonical-bits md5, NaN count,
+    sampled rows, max colour and PPM md5 (C5's whole frame from
+    tests/golden/make_c5_full.py: the reference build over all 2160 rows)."""
     c = golden["configs"][name]
     if "fb_md5" not in c:
         pytest.skip("golden has no full frame for " + name)
