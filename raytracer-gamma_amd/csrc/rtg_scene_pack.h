@@ -554,9 +554,6 @@ inline void cone_masks(const rtg_sphere* spheres, unsigned n, std::vector<unsign
   }
 }
 
-// RTG_BVH_HOMOG (rtg_trace.h): every node is either an inner node (child
-// boxes only) or a leaf (sphere slots only, at most 4 spheres; an empty slot
-// holds a far dummy sphere whose screen never passes).
 // 4-wide BVH of axis-aligned boxes (the queries are closest_bvh, blocked_bvh
 // and container_bvh in rtg_trace.h).  Each sphere gets a grown box (bvh_grow
 // below: every point the reference's root test can accept, and its
@@ -711,14 +708,9 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     }
     unsigned g[5];
     const unsigned cnt = hi - lo;
-    const bool leafNode = cnt <= 4;
-    if (leafNode) {
+    if (cnt <= 4) {
       for (unsigned k = 0; k <= cnt; ++k) g[k] = lo + k;
       for (unsigned k = cnt + 1; k <= 4; ++k) g[k] = hi;
-    } else if (RTG_BVH_HOMOG && cnt <= 8) {  // two leaves
-      g[0] = lo;
-      g[1] = split(lo, hi);
-      g[2] = g[3] = g[4] = hi;
     } else {
       g[0] = lo;
       g[4] = hi;
@@ -728,21 +720,10 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     }
     for (int k = 0; k < 4; ++k) {
       const unsigned a = g[k], b = g[k + 1];
-      if (a >= b) {
-        if (RTG_BVH_HOMOG && leafNode) {
-          // an empty sphere slot of a leaf: a far dummy record whose screen
-          // never passes (screen r^2 -inf), child 0, no containment
-          float* rec = &ps->bvhNodes[(size_t)node * kBvhWords];
-          rec[6 * k + 0] = rec[6 * k + 1] = rec[6 * k + 2] = 0x1p60f;
-          rec[6 * k + 3] = -__builtin_inff();
-          rec[6 * k + 4] = 0.f;
-          rec[6 * k + 5] = 0.f;
-        }
-        continue;
-      }
+      if (a >= b) continue;
       int child;
       float s[6], cr = -1.f;
-      if (RTG_BVH_HOMOG ? leafNode : b - a == 1) {
+      if (b - a == 1) {
         const unsigned i = idx[a];
         const rtg_sphere& sp = spheres[i];
         s[0] = sp.pos.x; s[1] = sp.pos.y; s[2] = sp.pos.z;

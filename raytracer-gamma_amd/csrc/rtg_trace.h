@@ -1434,14 +1434,6 @@ struct BvhRec {
   int ch[4];
   float cr[4];
 };
-// RTG_BVH_HOMOG (default 1; build_bvh): a node is an inner node (child boxes
-// only, ch[0] > 0) or a leaf (sphere slots only, ch[0] < 0; an empty slot is a
-// far dummy sphere with screen r^2 -inf and child 0), so a visit branches once
-// on its kind and its four slots run without per-slot dispatch: the waves are
-// scalar-issue bound.  0: the round-3 mixed nodes.
-#ifndef RTG_BVH_HOMOG
-#define RTG_BVH_HOMOG 1
-#endif
 
 // Children of a node for the wave: of the valid (child, key) pairs, keys =
 // a lane's box entry parameter (wave-uniform), the nearest is returned (the
@@ -1529,43 +1521,6 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
   {
     const unsigned u = 0xFFFFFFFFu;
     memcpy(&keyMax, &u, 4);
-  }
-  if (RTG_BVH_HOMOG) {
-    if (r.ch[0] < 0) {  // a leaf: four sphere slots (dummies never pass the screen)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        sc.count(kUBvhSlot, 1);
-        sc.count(shadowQ ? kCntBvhShadowSphereTests : kCntBvhSphereTests, 1);
-        const float* g = &r.s[6 * k];
-        const V3 c = v3(g[0], g[1], g[2]);
-        const V3 p = vsub(q.o, c);
-        const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
-        const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-        const float cs = p2 - g[3];
-        const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-        if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
-            !behind(0.5f * q.den, xd, cs, g[3]))
-          leaf((unsigned)~r.ch[k], c, g[4]);
-      }
-      return 0;
-    }
-    // an inner node: four box slots without branches (an empty slot has child
-    // 0: never valid, keyed last)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int x = r.ch[k];
-      sc.count(kUBvhSlot, 1);
-      sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
-      const float* g = &r.s[6 * k];
-      float tn;
-      const bool pass = active && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]),
-                                            reachT, tn);
-      if (pass) sc.count(kUBvhPass, 1);
-      const bool take = sc.any(pass) && x > 0;
-      pc[k] = take ? x : 0;
-      pk[k] = take ? sc.first_lane(tn) : keyMax;
-    }
-    return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -1689,35 +1644,6 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
     BvhRec r;
     sc.bvh_rec(nd, r);
     int nxt = 0;
-    if (RTG_BVH_HOMOG) {
-      if (r.ch[0] < 0) {  // a leaf (dummy slots: containment radius^2 -1)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float* g = &r.s[6 * k];
-          const V3 dist = vsub(pt, v3(g[0], g[1], g[2]));
-          if (vdot(dist, dist) <= r.cr[k] && (int)~r.ch[k] < found) found = (int)~r.ch[k];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int x = r.ch[k];
-          const float* g = &r.s[6 * k];
-          const bool in = pt.x >= g[0] && pt.y >= g[1] && pt.z >= g[2] && pt.x <= g[3] &&
-                          pt.y <= g[4] && pt.z <= g[5];
-          if (sc.any(in) && x > 0) {  // the last such child is the next node
-            if (nxt > 0) st.push(nxt);
-            nxt = x;
-          }
-        }
-      }
-      if (nxt > 0) {
-        nd = (unsigned)nxt;
-      } else {
-        if (st.empty()) break;
-        nd = (unsigned)st.pop();
-      }
-      continue;
-    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int x = r.ch[k];
