@@ -1453,6 +1453,9 @@ struct BvhRec {
 #ifndef RTG_BOX_SEL  // bvh_ray_node: a passing child box taken by selects, not a branch
 #define RTG_BOX_SEL 0
 #endif
+#ifndef RTG_LIST_PAIR  // list loops: both records of a pair, one exit test per pair
+#define RTG_LIST_PAIR 0
+#endif
 RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2, float f2,
                        int c3, float f3) {
   auto bits = [](float f) {
@@ -1716,8 +1719,15 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
     ListRec r0, r1;
     sc.cap_rec2(k, r0, r1);
     step(r0);
-    if (sc.all(blk) || k + 1 >= k1) break;
-    step(r1);
+    if (RTG_LIST_PAIR) {
+      // the pair's second record past the list's end is the next list's (or
+      // the table's padding record): a real sphere can only block if it
+      // blocks, so testing it keeps the answer; one exit test per pair
+      step(r1);
+    } else {
+      if (sc.all(blk) || k + 1 >= k1) break;
+      step(r1);
+    }
     if (sc.all(blk)) break;
   }
   return blk;
@@ -1759,7 +1769,10 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
     ListRec r0, r1;
     sc.ov_rec2(k, r0, r1);
     step(r0);
-    if (k + 1 < k1) step(r1);
+    // past the list's end: the next list's sphere (or the padding record);
+    // the answer is the lexicographic minimum over every sphere, so a real
+    // extra sphere keeps it
+    if (RTG_LIST_PAIR || k + 1 < k1) step(r1);
   }
   tOut = minT;
   return best;
@@ -1868,8 +1881,14 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
     ListRec r0, r1;
     sc.ov_rec2(k, r0, r1);
     step(r0);
-    if (sc.all(found >= 0) || k + 1 >= k1) break;
-    step(r1);
+    if (RTG_LIST_PAIR) {
+      // a sphere past the list's end (the next list's) cannot contain the
+      // point (primary_container_sel's argument: every container is listed)
+      step(r1);
+    } else {
+      if (sc.all(found >= 0) || k + 1 >= k1) break;
+      step(r1);
+    }
     if (sc.all(found >= 0)) break;
   }
   return found;
