@@ -1444,7 +1444,7 @@ struct BvhRec {
 // values (a -0 would sort last; the order only decides which node is visited
 // first, never an answer), so the compare-exchanges are scalar integer work.
 // The waves are scalar-issue bound (an extra scalar instruction per node
-// costs 2.4 times an extra vector one, DESIGN.md §4 item 46): a full
+// costs 2.4 times an extra vector one, DESIGN.md §4 item 45): a full
 // five-exchange sort visited 1 % fewer nodes and ran C5 4 % slower
 // (RTG_BVH_SORT=0, A/B builds).
 #ifndef RTG_BVH_SORT
