@@ -1563,6 +1563,36 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
 }
 
+// Closest-hit and shadow updates for an accepted root, as selects: the
+// exact (t, index) order and the reference's |t D|^2 < gap test, with no
+// exec-mask branch (each one costs scalar issue, DESIGN item 47).
+#ifndef RTG_SEL_UPD
+#define RTG_SEL_UPD 0
+#endif
+RTG_HD void take_closer(bool res, float t, int i, float& minT, int& best) {
+#if RTG_SEL_UPD
+  const bool b = res & ((t < minT) | ((t == minT) & (i < best)));
+  minT = b ? t : minT;
+  best = b ? i : best;
+#else
+  if (res && (t < minT || (t == minT && i < best))) {
+    minT = t;
+    best = i;
+  }
+#endif
+}
+RTG_HD void take_blocker(bool res, float t, V3 d, float gap, bool& blk) {
+#if RTG_SEL_UPD
+  const V3 dist = vsmul(t, d);
+  blk = blk | (res & (t < 1000.f) & (vdot(dist, dist) < gap));
+#else
+  if (res && t < 1000.f) {
+    const V3 dist = vsmul(t, d);
+    if (vdot(dist, dist) < gap) blk = true;
+  }
+#endif
+}
+
 // (minT0, best0): a candidate already known (an accepted root of sphere
 // best0, or 1000 / -1): the answer is the lexicographic minimum of (t, i)
 // over every accepted root below 1000, so starting from any real candidate
@@ -1584,10 +1614,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
       sc.count(kUBvhExact, 1);
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
-      if (res && (t < minT || (t == minT && (int)i < best))) {
-        minT = t;
-        best = (int)i;
-      }
+      take_closer(res, t, (int)i, minT, best);
     });
     if (nx > 0) {
       nd = (unsigned)nx;
@@ -1621,10 +1648,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       sc.count(kUBvhExact, 1);
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
-      if (res && t < 1000.f) {
-        const V3 dist = vsmul(t, q.d);
-        if (vdot(dist, dist) < gap) blk = true;
-      }
+      take_blocker(res, t, q.d, gap, blk);
     }, true);
     if (sc.all(blk)) break;
     if (nx > 0) {
@@ -1706,10 +1730,7 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
       sc.count(kUShdExact, 1);
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
-      if (res && t < 1000.f) {
-        const V3 dist = vsmul(t, q.d);
-        if (vdot(dist, dist) < gap) blk = true;
-      }
+      take_blocker(res, t, q.d, gap, blk);
     }
   };
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
@@ -1759,7 +1780,7 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
       sc.count(kUEnterExact, 1);
       bool rj;
       const float t = ray_sphere_leaf(q, r.c, r.r2, rj);
-      if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
+      take_closer(rj, t, j, minT, best);
     }
   };
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
@@ -1807,7 +1828,7 @@ RTG_HD int closest_near(const Scene& sc, const RayQ& q, int h, float& tOut) {
       bool rj;
       const float t = ray_sphere(q, r.c, r.r2, rj);
       const int j = r.idx;
-      if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
+      take_closer(rj, t, j, minT, best);
     }
   };
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
@@ -1844,7 +1865,7 @@ RTG_HD int closest_seeded(const Scene& sc, const RayQ& q, int h, float& tOut) {
       bool rj;
       const float t = ray_sphere(q, r.c, r.r2, rj);
       const int j = r.idx;
-      if (rj && (t < minT || (t == minT && j < best))) { minT = t; best = j; }
+      take_closer(rj, t, j, minT, best);
     }
   };
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
