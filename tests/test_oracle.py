@@ -121,14 +121,18 @@ def hostsim():
     if ASAN:  # tests/asan/Makefile build (tests/test_sanitizers.py)
         return ctypes.CDLL(os.path.join(ASAN_BUILD, "libhostsim.so"))
     os.makedirs(BUILD, exist_ok=True)
-    so = os.path.join(BUILD, "libhostsim.so")
+    # RTG_HOSTSIM_DEFS="-DRTG_X=1 ...": an A/B knob's host build, for the
+    # parity tests of a trial before it is adopted (DESIGN item 37)
+    defs = os.environ.get("RTG_HOSTSIM_DEFS", "").split()
+    tag = "".join(c for c in "_".join(defs) if c.isalnum() or c == "_")
+    so = os.path.join(BUILD, "libhostsim%s.so" % (("_" + tag) if tag else ""))
     src = os.path.join(ROOT, "tests", "hostsim", "hostsim.cpp")
     deps = [src, os.path.abspath(__file__)] + [
         os.path.join(ROOT, "raytracer-gamma_amd", "csrc", f) for f in
         ("rtg_trace.h", "rtg_scene_pack.h", "rtg_internal.h")]
     if not os.path.exists(so) or any(os.path.getmtime(d) > os.path.getmtime(so) for d in deps):
         subprocess.run(["g++", "-O2", "-mfma", "-ffp-contract=off", "-fno-fast-math", "-std=c++17",
-                        "-fPIC", "-shared", "-I" + os.path.join(ROOT, "include"),
+                        "-fPIC", "-shared", *defs, "-I" + os.path.join(ROOT, "include"),
                         "-I" + os.path.join(ROOT, "raytracer-gamma_amd", "csrc"), src, "-o", so],
                        check=True)
     return ctypes.CDLL(so)
