@@ -372,6 +372,21 @@ RTG_HD float quot(float x, const RayQ& q) {
   return r;
 }
 
+// The same with the quotient path chosen for the whole wave (kFast: every
+// lane's denominator is in the Markstein range, all(q.fast)).
+template <bool kFast>
+RTG_HD float quot_k(float x, const RayQ& q) {
+  if constexpr (kFast) {
+    const float q0 = x * q.y;
+    const float r0 = fmaf(-q0, q.den, x);
+    const float q1 = fmaf(r0, q.y, q0);
+    const float r1 = fmaf(-q1, q.den, x);
+    return fmaf(r1, q.y, q1);
+  } else {
+    return quot(x, q);
+  }
+}
+
 // No root of the reference's test can be accepted (raytracer.h:105-138)
 // when, in its own values b and cc, b > 0 and b < 16 a and either cc >= 0
 // (the origin outside and the centre behind it: radicand <= fl(b b), so
@@ -399,6 +414,11 @@ RTG_HD bool no_root(const RayQ& q, float b, float cc) {
 // Per-sphere ray test, raytracer.h:81-141.  Returns the smallest root in
 // (1e-5, 10000) or 10000 when none (`res` tells).  kNone: lanes where
 // no_root holds skip the roots (same answer).
+// RTG_QUOT2=1 (A/B builds): both quotients' division fallback in one
+// wave-uniform branch instead of one each (same values).
+#ifndef RTG_QUOT2
+#define RTG_QUOT2 0
+#endif
 template <bool kNone = false>
 RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   V3 disp = vsub(q.o, c);
@@ -409,8 +429,21 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   res = false;
   if (radicand >= 0.0f && !(kNone && no_root(q, b, cc))) {
     const float root = rtg_sqrtf(radicand);
+#if RTG_QUOT2
+    const float x0 = -b + root, x1 = -b - root;
+    float u0 = quot_k<true>(x0, q);
+    float u1 = quot_k<true>(x1, q);
+    if (q.slow) {
+      no_speculate();
+      if (!q.fast) {
+        u0 = x0 / q.den;
+        u1 = x1 / q.den;
+      }
+    }
+#else
     const float u0 = quot(-b + root, q);
     const float u1 = quot(-b - root, q);
+#endif
     if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
     if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
   }
@@ -449,21 +482,6 @@ template <bool kNone = false>
 RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res) {
   if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);
   return ray_sphere<kNone>(q, c, r2, res);
-}
-
-// The same with the quotient path chosen for the whole wave (kFast: every
-// lane's denominator is in the Markstein range, all(q.fast)).
-template <bool kFast>
-RTG_HD float quot_k(float x, const RayQ& q) {
-  if constexpr (kFast) {
-    const float q0 = x * q.y;
-    const float r0 = fmaf(-q0, q.den, x);
-    const float q1 = fmaf(r0, q.y, q0);
-    const float r1 = fmaf(-q1, q.den, x);
-    return fmaf(r1, q.y, q1);
-  } else {
-    return quot(x, q);
-  }
 }
 
 template <bool kFast, bool kNone = false>
