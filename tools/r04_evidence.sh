@@ -37,6 +37,11 @@ for c in ${CONFIGS:-c3 c2 c4 c5 c1cpu}; do
   timeout -k 10 600 python bench.py --config $c --steps ${STEPS:-20} --warmup 3 ${BENCH_ARGS:-} > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { tail -5 $OUT/bench_$c.err; exit 1; }
   python -c "import json;d=json.loads(open('$OUT/bench_$c.json').read().strip().splitlines()[-1]);r=d['roofline'] or {};print('$c', d['value'], d['unit'], d['ms_per_step'], 'first', d.get('first_launch_ms'), 'frac', r.get('frac'), 'cpu', (d['cpu_baseline'] or {}).get('value'), 'bit_exact', d['parity'].get('bit_exact'), 'fb', d['parity'].get('fb_md5_match'), 'ppm', d['parity'].get('ppm_md5_match'), 'e2e', (d['e2e'] or {}).get('e2e_ms'))"
 done
+if [ -n "$CHUNKS" ]; then
+  echo "== chunk rehearsal c3/c4 (8-GPU prediction inputs)" &&
+  timeout -k 10 300 python tools/chunk_rehearsal.py --config c3 --ranks 2,4,8 --chunks 1,3,4 --last-frac 0.15 --json $OUT/chunks_c3.json > $OUT/chunks_c3.txt 2>&1 && tail -8 $OUT/chunks_c3.txt &&
+  timeout -k 10 300 python tools/chunk_rehearsal.py --config c4 --ranks 8 --chunks 1,3 --last-frac 0.15 --json $OUT/chunks_c4.json > $OUT/chunks_c4.txt 2>&1 && tail -4 $OUT/chunks_c4.txt || exit 1
+fi
 [ -n "$NO_PROFILES" ] && exit 0
 echo "== rocprofv3 kernel trace (c3 bench)" &&
 ( cd /tmp && export TMPDIR=/tmp &&
