@@ -419,15 +419,16 @@ RTG_HD bool no_root(const RayQ& q, float b, float cc) {
 #ifndef RTG_QUOT2
 #define RTG_QUOT2 0
 #endif
+// `skip`: the lane is known to have no accepted root (behind, late form).
 template <bool kNone = false>
-RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
+RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res, bool skip = false) {
   V3 disp = vsub(q.o, c);
   const float b = 2.0f * vdot(q.d, disp);
   const float cc = vdot(disp, disp) - r2;
   const float radicand = (b * b) - (q.a4 * cc);
   float sm = 10000.f;
   res = false;
-  if (radicand >= 0.0f && !(kNone && no_root(q, b, cc))) {
+  if (radicand >= 0.0f && !skip && !(kNone && no_root(q, b, cc))) {
     const float root = rtg_sqrtf(radicand);
 #if RTG_QUOT2
     const float x0 = -b + root, x1 = -b - root;
@@ -479,9 +480,9 @@ RTG_HD float ray_sphere_sel(const RayQ& q, V3 c, float r2, bool& res) {
   return sm;
 }
 template <bool kNone = false>
-RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res) {
-  if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);
-  return ray_sphere<kNone>(q, c, r2, res);
+RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res, bool skip = false) {
+  if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);  // (probe builds: no skip)
+  return ray_sphere<kNone>(q, c, r2, res, skip);
 }
 
 template <bool kFast, bool kNone = false>
@@ -1291,11 +1292,23 @@ RTG_HD bool behind(float a, float x, float cs, float rs) {
 }
 // pass1_rad's screen and `behind` in one: false when sphere (c, rs) can have
 // no accepted root.
-RTG_HD bool screen_ahead(const RayQ& q, V3 c, float rs) {
+// RTG_BEHIND_LATE=1 (A/B builds): `behind` is folded into the exact test's
+// radicand condition (`bh`, the skip argument of ray_sphere) instead of a
+// region of its own: one exec-mask save/branch/restore less per screened
+// sphere, the radicand computed for waves whose lanes are all behind.
+#ifndef RTG_BEHIND_LATE
+#define RTG_BEHIND_LATE 0
+#endif
+RTG_HD bool screen_ahead(const RayQ& q, V3 c, float rs, bool& bh) {
   const V3 p = vsub(q.o, c);
   const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
   const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rs)));
   const float v = fmaf(x, x, fmaf(-q.ap, cs, 0x1p-100f));
+  if (RTG_BEHIND_LATE) {
+    bh = behind(0.5f * q.den, x, cs, rs);
+    return !(v < 0.f);
+  }
+  bh = false;
   return !(v < 0.f) && !behind(0.5f * q.den, x, cs, rs);
 }
 
@@ -1518,7 +1531,8 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2,
 // ray parameter units) and distance pruning + pass-1 screens of its sphere
 // slots (reach `reachD` in distance units); child nodes some active lane
 // still needs are ordered front to back (the nearest returned, the others
-// pushed), sphere slots are handed to `leaf(i, c, r2)` for lanes that pass.
+// pushed), sphere slots are handed to `leaf(i, c, r2, bh)` for lanes that
+// pass (bh: `behind` in its late form, RTG_BEHIND_LATE).
 // `active`: the lane still queries.  Returns the next node (> 0) or 0.
 template <class Scene, class Leaf>
 RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
@@ -1573,9 +1587,13 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
       const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
       const float cs = p2 - g[3];
       const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-      if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
-          !behind(0.5f * q.den, xd, cs, g[3]))
-        leaf((unsigned)~x, c, g[4]);
+      if (RTG_BEHIND_LATE) {
+        if (active && !beyond(p2, g[5], reachD) && !(v < 0.f))
+          leaf((unsigned)~x, c, g[4], behind(0.5f * q.den, xd, cs, g[3]));
+      } else if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
+                 !behind(0.5f * q.den, xd, cs, g[3])) {
+        leaf((unsigned)~x, c, g[4], false);
+      }
     }
   }
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
@@ -1627,11 +1645,11 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
     const int nx = bvh_ray_node(sc, q, b, nd, active, minT, minT * dn, st,
-                                [&](unsigned i, V3 ce, float r2) {
+                                [&](unsigned i, V3 ce, float r2, bool bh) {
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res, bh);
       take_closer(res, t, (int)i, minT, best);
     });
     if (nx > 0) {
@@ -1661,11 +1679,11 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
     const int nx = bvh_ray_node(sc, q, b, nd, !blk, reachT, reachD, st,
-                                [&](unsigned, V3 ce, float r2) {
+                                [&](unsigned, V3 ce, float r2, bool bh) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res, bh);
       take_blocker(res, t, q.d, gap, blk);
     }, true);
     if (sc.all(blk)) break;
@@ -1744,10 +1762,11 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
   bool blk = false;
   auto step = [&](const ListRec& r) {
     sc.count(kUCapIter, 1);
-    if (!blk && screen_ahead(q, r.c, r.rs)) {
+    bool bh;
+    if (!blk && screen_ahead(q, r.c, r.rs, bh)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res, bh);
       take_blocker(res, t, q.d, gap, blk);
     }
   };
@@ -1794,10 +1813,11 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
     const int j = r.idx;
     if (j == h) return;
     sc.count(kUOvIter, 1);
-    if (screen_ahead(q, r.c, r.rs)) {
+    bool bh;
+    if (screen_ahead(q, r.c, r.rs, bh)) {
       sc.count(kUEnterExact, 1);
       bool rj;
-      const float t = ray_sphere_leaf(q, r.c, r.r2, rj);
+      const float t = ray_sphere_leaf(q, r.c, r.r2, rj, bh);
       take_closer(rj, t, j, minT, best);
     }
   };
@@ -1841,10 +1861,11 @@ RTG_HD int closest_near(const Scene& sc, const RayQ& q, int h, float& tOut) {
       return;
     }
     sc.count(kUNbrIter, 1);
-    if (screen_ahead(q, r.c, r.rs)) {
+    bool bh;
+    if (screen_ahead(q, r.c, r.rs, bh)) {
       sc.count(kUBvhExact, 1);
       bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj);
+      const float t = ray_sphere(q, r.c, r.r2, rj, bh);
       const int j = r.idx;
       take_closer(rj, t, j, minT, best);
     }
@@ -1878,10 +1899,11 @@ RTG_HD int closest_seeded(const Scene& sc, const RayQ& q, int h, float& tOut) {
   sc.ov_range((unsigned)h, k0, k1);
   auto step = [&](const ListRec& r) {
     sc.count(kUOvIter, 1);
-    if (screen_ahead(q, r.c, r.rs)) {
+    bool bh;
+    if (screen_ahead(q, r.c, r.rs, bh)) {
       sc.count(kUBvhExact, 1);
       bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj);
+      const float t = ray_sphere(q, r.c, r.r2, rj, bh);
       const int j = r.idx;
       take_closer(rj, t, j, minT, best);
     }
