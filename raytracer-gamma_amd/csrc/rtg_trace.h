@@ -1488,6 +1488,14 @@ struct BvhRec {
 #ifndef RTG_LIST_PAIR
 #define RTG_LIST_PAIR 1
 #endif
+// RTG_NODE_SPLIT=1 (A/B builds): a node's sphere slots in one unrolled pass
+// and its box slots in a second, each slot behind one wave-uniform test of
+// its child word, instead of one pass that tests empty / box / sphere (its
+// if/else costs the structurizer's flow instructions per slot).  The box
+// tests take the node's entry reach either way, so the order changes nothing.
+#ifndef RTG_NODE_SPLIT
+#define RTG_NODE_SPLIT 0
+#endif
 RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2, float f2,
                        int c3, float f3) {
   auto bits = [](float f) {
@@ -1561,39 +1569,56 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     const unsigned u = 0xFFFFFFFFu;
     memcpy(&keyMax, &u, 4);
   }
+  auto box_slot = [&](int k, int x) {
+    const float* g = &r.s[6 * k];
+    sc.count(kUBvhSlot, 1);
+    sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
+    float tn;
+    const bool pass = active && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]),
+                                          reachT, tn);
+    if (pass) sc.count(kUBvhPass, 1);
+    if (sc.any(pass)) {
+      pc[k] = x;
+      pk[k] = sc.first_lane(tn);
+    }
+  };
+  auto sphere_slot = [&](int k, int x) {
+    const float* g = &r.s[6 * k];
+    sc.count(kUBvhSlot, 1);
+    sc.count(shadowQ ? kCntBvhShadowSphereTests : kCntBvhSphereTests, 1);
+    const V3 c = v3(g[0], g[1], g[2]);
+    const V3 p = vsub(q.o, c);
+    const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
+    const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
+    const float cs = p2 - g[3];
+    const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
+    if (RTG_BEHIND_LATE) {
+      if (active && !beyond(p2, g[5], reachD) && !(v < 0.f))
+        leaf((unsigned)~x, c, g[4], behind(0.5f * q.den, xd, cs, g[3]));
+    } else if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
+               !behind(0.5f * q.den, xd, cs, g[3])) {
+      leaf((unsigned)~x, c, g[4], false);
+    }
+  };
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     pc[k] = 0;
     pk[k] = keyMax;
-    const int x = r.ch[k];
-    if (x == 0) continue;  // wave-uniform
-    sc.count(kUBvhSlot, 1);
-    const float* g = &r.s[6 * k];
-    if (x > 0) {
-      sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
-      float tn;
-      const bool pass = active && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]),
-                                            reachT, tn);
-      if (pass) sc.count(kUBvhPass, 1);
-      if (sc.any(pass)) {
-        pc[k] = x;
-        pk[k] = sc.first_lane(tn);
-      }
-    } else {
-      sc.count(shadowQ ? kCntBvhShadowSphereTests : kCntBvhSphereTests, 1);
-      const V3 c = v3(g[0], g[1], g[2]);
-      const V3 p = vsub(q.o, c);
-      const float xd = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
-      const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-      const float cs = p2 - g[3];
-      const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-      if (RTG_BEHIND_LATE) {
-        if (active && !beyond(p2, g[5], reachD) && !(v < 0.f))
-          leaf((unsigned)~x, c, g[4], behind(0.5f * q.den, xd, cs, g[3]));
-      } else if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
-                 !behind(0.5f * q.den, xd, cs, g[3])) {
-        leaf((unsigned)~x, c, g[4], false);
-      }
+  }
+  if (RTG_NODE_SPLIT) {  // sphere slots, then box slots: one test per slot and pass
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r.ch[k] < 0) sphere_slot(k, r.ch[k]);  // wave-uniform
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r.ch[k] > 0) box_slot(k, r.ch[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = r.ch[k];
+      if (x == 0) continue;  // wave-uniform
+      if (x > 0) box_slot(k, x);
+      else sphere_slot(k, x);
     }
   }
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
