@@ -1493,12 +1493,6 @@ struct BvhRec {
 // its child word, instead of one pass that tests empty / box / sphere (its
 // if/else costs the structurizer's flow instructions per slot).  The box
 // tests take the node's entry reach either way, so the order changes nothing.
-// RTG_KEY_PASS=1 (A/B builds): a child's sort key is the entry parameter of
-// the first lane whose ray passes its box, not of the wave's first lane
-// (which may miss it: its key then orders nothing); one s_ff1 more per child.
-#ifndef RTG_KEY_PASS
-#define RTG_KEY_PASS 0
-#endif
 #ifndef RTG_NODE_SPLIT
 #define RTG_NODE_SPLIT 0
 #endif
@@ -1585,7 +1579,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     if (pass) sc.count(kUBvhPass, 1);
     if (sc.any(pass)) {
       pc[k] = x;
-      pk[k] = RTG_KEY_PASS ? sc.first_pass_lane(pass, tn) : sc.first_lane(tn);
+      pk[k] = sc.first_lane(tn);
     }
   };
   auto sphere_slot = [&](int k, int x) {

@@ -352,11 +352,6 @@ struct DevScene {
   __device__ __forceinline__ int first_lane_i(int v) const {
     return __builtin_amdgcn_readfirstlane(v);
   }
-  // v of the first lane where `pass` holds (some lane must hold it).
-  __device__ __forceinline__ float first_pass_lane(bool pass, float v) const {
-    const int l = (int)__builtin_ctzll(__ballot(pass));
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-  }
   __device__ __forceinline__ V3 first_lane(V3 v) const {
     return v3(first_lane(v.x), first_lane(v.y), first_lane(v.z));
   }

@@ -99,7 +99,6 @@ struct HostScene {
   }
   float first_lane(float v) const { return v; }
   int first_lane_i(int v) const { return v; }
-  float first_pass_lane(bool, float v) const { return v; }
   rtg::V3 sphere(unsigned i, float& r2) const {
     const float* g = geom + 4 * i;
     r2 = g[3];
