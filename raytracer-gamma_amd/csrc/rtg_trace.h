@@ -414,21 +414,20 @@ RTG_HD bool no_root(const RayQ& q, float b, float cc) {
 // Per-sphere ray test, raytracer.h:81-141.  Returns the smallest root in
 // (1e-5, 10000) or 10000 when none (`res` tells).  kNone: lanes where
 // no_root holds skip the roots (same answer).
-// RTG_QUOT2=1 (A/B builds): both quotients' division fallback in one
-// wave-uniform branch instead of one each (same values).
+// Both quotients' division fallback in one wave-uniform branch instead of
+// one each (same values; RTG_QUOT2=0: one each).
 #ifndef RTG_QUOT2
-#define RTG_QUOT2 0
+#define RTG_QUOT2 1
 #endif
-// `skip`: the lane is known to have no accepted root (behind, late form).
 template <bool kNone = false>
-RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res, bool skip = false) {
+RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   V3 disp = vsub(q.o, c);
   const float b = 2.0f * vdot(q.d, disp);
   const float cc = vdot(disp, disp) - r2;
   const float radicand = (b * b) - (q.a4 * cc);
   float sm = 10000.f;
   res = false;
-  if (radicand >= 0.0f && !skip && !(kNone && no_root(q, b, cc))) {
+  if (radicand >= 0.0f && !(kNone && no_root(q, b, cc))) {
     const float root = rtg_sqrtf(radicand);
 #if RTG_QUOT2
     const float x0 = -b + root, x1 = -b - root;
@@ -480,9 +479,9 @@ RTG_HD float ray_sphere_sel(const RayQ& q, V3 c, float r2, bool& res) {
   return sm;
 }
 template <bool kNone = false>
-RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res, bool skip = false) {
-  if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);  // (probe builds: no skip)
-  return ray_sphere<kNone>(q, c, r2, res, skip);
+RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res) {
+  if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);
+  return ray_sphere<kNone>(q, c, r2, res);
 }
 
 template <bool kFast, bool kNone = false>
@@ -1292,23 +1291,11 @@ RTG_HD bool behind(float a, float x, float cs, float rs) {
 }
 // pass1_rad's screen and `behind` in one: false when sphere (c, rs) can have
 // no accepted root.
-// RTG_BEHIND_LATE=1 (A/B builds): `behind` is folded into the exact test's
-// radicand condition (`bh`, the skip argument of ray_sphere) instead of a
-// region of its own: one exec-mask save/branch/restore less per screened
-// sphere, the radicand computed for waves whose lanes are all behind.
-#ifndef RTG_BEHIND_LATE
-#define RTG_BEHIND_LATE 0
-#endif
-RTG_HD bool screen_ahead(const RayQ& q, V3 c, float rs, bool& bh) {
+RTG_HD bool screen_ahead(const RayQ& q, V3 c, float rs) {
   const V3 p = vsub(q.o, c);
   const float x = fmaf(q.d.x, p.x, fmaf(q.d.y, p.y, q.d.z * p.z));
   const float cs = fmaf(p.x, p.x, fmaf(p.y, p.y, fmaf(p.z, p.z, -rs)));
   const float v = fmaf(x, x, fmaf(-q.ap, cs, 0x1p-100f));
-  if (RTG_BEHIND_LATE) {
-    bh = behind(0.5f * q.den, x, cs, rs);
-    return !(v < 0.f);
-  }
-  bh = false;
   return !(v < 0.f) && !behind(0.5f * q.den, x, cs, rs);
 }
 
@@ -1488,13 +1475,14 @@ struct BvhRec {
 #ifndef RTG_LIST_PAIR
 #define RTG_LIST_PAIR 1
 #endif
-// RTG_NODE_SPLIT=1 (A/B builds): a node's sphere slots in one unrolled pass
-// and its box slots in a second, each slot behind one wave-uniform test of
-// its child word, instead of one pass that tests empty / box / sphere (its
-// if/else costs the structurizer's flow instructions per slot).  The box
-// tests take the node's entry reach either way, so the order changes nothing.
+// A node's sphere slots in one unrolled pass and its box slots in a second,
+// each slot behind one wave-uniform test of its child word, instead of one
+// pass that tests empty / box / sphere, whose if/else costs the
+// structurizer's flow instructions per slot (RTG_NODE_SPLIT=0; C5 -3.1 %,
+// DESIGN.md §4 item 48).  The box tests take the node's entry reach either
+// way, so the order changes nothing.
 #ifndef RTG_NODE_SPLIT
-#define RTG_NODE_SPLIT 0
+#define RTG_NODE_SPLIT 1
 #endif
 RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2, float f2,
                        int c3, float f3) {
@@ -1539,8 +1527,7 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2,
 // ray parameter units) and distance pruning + pass-1 screens of its sphere
 // slots (reach `reachD` in distance units); child nodes some active lane
 // still needs are ordered front to back (the nearest returned, the others
-// pushed), sphere slots are handed to `leaf(i, c, r2, bh)` for lanes that
-// pass (bh: `behind` in its late form, RTG_BEHIND_LATE).
+// pushed), sphere slots are handed to `leaf(i, c, r2)` for lanes that pass.
 // `active`: the lane still queries.  Returns the next node (> 0) or 0.
 template <class Scene, class Leaf>
 RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
@@ -1592,13 +1579,9 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
     const float cs = p2 - g[3];
     const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-    if (RTG_BEHIND_LATE) {
-      if (active && !beyond(p2, g[5], reachD) && !(v < 0.f))
-        leaf((unsigned)~x, c, g[4], behind(0.5f * q.den, xd, cs, g[3]));
-    } else if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
-               !behind(0.5f * q.den, xd, cs, g[3])) {
-      leaf((unsigned)~x, c, g[4], false);
-    }
+    if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
+        !behind(0.5f * q.den, xd, cs, g[3]))
+      leaf((unsigned)~x, c, g[4]);
   };
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -1624,11 +1607,12 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
 }
 
-// Closest-hit and shadow updates for an accepted root, as selects: the
-// exact (t, index) order and the reference's |t D|^2 < gap test, with no
-// exec-mask branch (each one costs scalar issue, DESIGN item 47).
+// Closest-hit and shadow updates for an accepted root (BVH and list loops),
+// as selects: the exact (t, index) order and the reference's |t D|^2 < gap
+// test with no exec-mask branch, whose save/branch/restore costs scalar issue
+// (RTG_SEL_UPD=0: branches; with RTG_QUOT2, C5 -3.2 %).
 #ifndef RTG_SEL_UPD
-#define RTG_SEL_UPD 0
+#define RTG_SEL_UPD 1
 #endif
 RTG_HD void take_closer(bool res, float t, int i, float& minT, int& best) {
 #if RTG_SEL_UPD
@@ -1670,11 +1654,11 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
     const int nx = bvh_ray_node(sc, q, b, nd, active, minT, minT * dn, st,
-                                [&](unsigned i, V3 ce, float r2, bool bh) {
+                                [&](unsigned i, V3 ce, float r2) {
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res, bh);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_closer(res, t, (int)i, minT, best);
     });
     if (nx > 0) {
@@ -1704,11 +1688,11 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
     const int nx = bvh_ray_node(sc, q, b, nd, !blk, reachT, reachD, st,
-                                [&](unsigned, V3 ce, float r2, bool bh) {
+                                [&](unsigned, V3 ce, float r2) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res, bh);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_blocker(res, t, q.d, gap, blk);
     }, true);
     if (sc.all(blk)) break;
@@ -1787,11 +1771,10 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
   bool blk = false;
   auto step = [&](const ListRec& r) {
     sc.count(kUCapIter, 1);
-    bool bh;
-    if (!blk && screen_ahead(q, r.c, r.rs, bh)) {
+    if (!blk && screen_ahead(q, r.c, r.rs)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res, bh);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
       take_blocker(res, t, q.d, gap, blk);
     }
   };
@@ -1838,11 +1821,10 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
     const int j = r.idx;
     if (j == h) return;
     sc.count(kUOvIter, 1);
-    bool bh;
-    if (screen_ahead(q, r.c, r.rs, bh)) {
+    if (screen_ahead(q, r.c, r.rs)) {
       sc.count(kUEnterExact, 1);
       bool rj;
-      const float t = ray_sphere_leaf(q, r.c, r.r2, rj, bh);
+      const float t = ray_sphere_leaf(q, r.c, r.r2, rj);
       take_closer(rj, t, j, minT, best);
     }
   };
@@ -1886,11 +1868,10 @@ RTG_HD int closest_near(const Scene& sc, const RayQ& q, int h, float& tOut) {
       return;
     }
     sc.count(kUNbrIter, 1);
-    bool bh;
-    if (screen_ahead(q, r.c, r.rs, bh)) {
+    if (screen_ahead(q, r.c, r.rs)) {
       sc.count(kUBvhExact, 1);
       bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj, bh);
+      const float t = ray_sphere(q, r.c, r.r2, rj);
       const int j = r.idx;
       take_closer(rj, t, j, minT, best);
     }
@@ -1924,11 +1905,10 @@ RTG_HD int closest_seeded(const Scene& sc, const RayQ& q, int h, float& tOut) {
   sc.ov_range((unsigned)h, k0, k1);
   auto step = [&](const ListRec& r) {
     sc.count(kUOvIter, 1);
-    bool bh;
-    if (screen_ahead(q, r.c, r.rs, bh)) {
+    if (screen_ahead(q, r.c, r.rs)) {
       sc.count(kUBvhExact, 1);
       bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj, bh);
+      const float t = ray_sphere(q, r.c, r.r2, rj);
       const int j = r.idx;
       take_closer(rj, t, j, minT, best);
     }
