@@ -67,12 +67,15 @@ def main():
     tr = stats([dur(t[1]) for t in timed])
     culls = [t[0] for t in timed if t[0] is not None]
     cu = stats([dur(c) for c in culls]) if culls else None
+    gaps = [int(t[1]["Start_Timestamp"]) - int(t[0]["End_Timestamp"]) for t in timed
+            if t[0] is not None]
     start = int((timed[0][0] or timed[0][1])["Start_Timestamp"])
     end = int(timed[-1][1]["End_Timestamp"])
     span_ms = (end - start) / count / 1e6
     out = {"bench": os.path.basename(bench_json), "config": bench["config"]["workload"],
            "timed_launches": [first, count], "trace_kernel": name, "trace": tr, "cull": cu,
            "frame_span_ms": round(span_ms, 4),
+           "cull_end_to_trace_start_us": round(sum(gaps) / len(gaps) / 1e3, 2) if gaps else None,
            "kernels_ms": round((tr["avg_ns"] + (cu["avg_ns"] if cu else 0)) / 1e6, 4),
            "bench_ms_per_step": bench["ms_per_step"], "bench_kernel_ms": bench["kernel_ms"],
            "first_launch_ms_bench": bench.get("first_launch_ms"),
