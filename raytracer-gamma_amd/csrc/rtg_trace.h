@@ -1638,25 +1638,13 @@ RTG_HD void take_blocker(bool res, float t, V3 d, float gap, bool& blk) {
 #endif
 }
 
-// RTG_BVH_FASTQ=1 (A/B builds): a BVH query whose lanes all have their
-// denominator in the Markstein range (!q.slow, wave-uniform) runs a copy of
-// the traversal whose root tests have no division fallback at all.
-#ifndef RTG_BVH_FASTQ
-#define RTG_BVH_FASTQ 0
-#endif
-template <bool kF, bool kNone>
-RTG_HD float bvh_leaf_test(const RayQ& q, V3 c, float r2, bool& res) {
-  if constexpr (kF) return ray_sphere_k<true, kNone>(q, c, r2, res);
-  else return ray_sphere_leaf<kNone>(q, c, r2, res);
-}
-
 // (minT0, best0): a candidate already known (an accepted root of sphere
 // best0, or 1000 / -1): the answer is the lexicographic minimum of (t, i)
 // over every accepted root below 1000, so starting from any real candidate
 // gives the same answer with a shorter reach (closest_seeded).
-template <bool kF, class Scene>
-RTG_HD int closest_bvh_k(const Scene& sc, const RayQ& q, float& tOut, float minT0, int best0,
-                         bool active) {
+template <class Scene>
+RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 = 1000.f,
+                       int best0 = -1, bool active = true) {
   float minT = minT0;
   int best = best0;
   const float dn = norm_up(q.den * 0.5f);
@@ -1670,7 +1658,7 @@ RTG_HD int closest_bvh_k(const Scene& sc, const RayQ& q, float& tOut, float minT
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = bvh_leaf_test<kF, (RTG_NOROOT >= 2)>(q, ce, r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_closer(res, t, (int)i, minT, best);
     });
     if (nx > 0) {
@@ -1683,18 +1671,12 @@ RTG_HD int closest_bvh_k(const Scene& sc, const RayQ& q, float& tOut, float minT
   tOut = minT;
   return best;
 }
-template <class Scene>
-RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 = 1000.f,
-                       int best0 = -1, bool active = true) {
-  if (RTG_BVH_FASTQ && !q.slow) return closest_bvh_k<true>(sc, q, tOut, minT0, best0, active);
-  return closest_bvh_k<false>(sc, q, tOut, minT0, best0, active);
-}
 
 // Shadow ray: blocked iff an accepted root t < 1000 has |t D|^2 < gap, so t
 // < sqrt(gap / a) (1 + 2^-18) covers the float test's rounding; a lane
 // outside the Markstein range (a tiny or huge) keeps the plain t < 1000.
-template <bool kF, class Scene>
-RTG_HD bool blocked_bvh_k(const Scene& sc, const RayQ& q, float gap) {
+template <class Scene>
+RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   bool blk = false;
   const float reachD = norm_up(gap);
   float reachT = sqrt_hw(gap * rcp_hw(q.den * 0.5f)) * (1.0f + 0x1p-18f);
@@ -1710,7 +1692,7 @@ RTG_HD bool blocked_bvh_k(const Scene& sc, const RayQ& q, float gap) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = bvh_leaf_test<kF, (RTG_NOROOT >= 2)>(q, ce, r2, res);
+      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_blocker(res, t, q.d, gap, blk);
     }, true);
     if (sc.all(blk)) break;
@@ -1722,11 +1704,6 @@ RTG_HD bool blocked_bvh_k(const Scene& sc, const RayQ& q, float gap) {
     }
   }
   return blk;
-}
-template <class Scene>
-RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
-  if (RTG_BVH_FASTQ && !q.slow) return blocked_bvh_k<true>(sc, q, gap);
-  return blocked_bvh_k<false>(sc, q, gap);
 }
 
 // Containment: a sphere's containment ball (r + 1e-6, raytracer.h:259-264,
