@@ -191,9 +191,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   // the previous launch's mean group time (ticks), 0: no feedback
   float mu = 0.f;
   if (a.costPrev != nullptr) {
-    unsigned long long st = 0;
-#pragma unroll
-    for (unsigned w = 0; w < kStatWays; ++w) st += a.costPrev[w * kStatStride];
+    const unsigned long long st = *a.costPrev;
     const unsigned ng = (unsigned)(st >> 40);
     if (ng != 0u) mu = (float)(st & ((1ull << 40) - 1ull)) / (float)ng;
   }
@@ -242,10 +240,10 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     unsigned sum = 0;
     for (unsigned k = 0; k < kCullRounds; ++k)
       for (unsigned w = 0; w < 4; ++w) sum += cnt[c][k][w];
-    blockBase[c] = sum ? atomicAdd(&groupCount[c * kCntStride], sum) : 0u;
+    blockBase[c] = sum ? atomicAdd(&groupCount[c], sum) : 0u;
   } else if (threadIdx.x == 64 && a.costStat != nullptr) {
     const unsigned long long t = waveCost[0] + waveCost[1] + waveCost[2] + waveCost[3];
-    if (t) atomicAdd(&a.costStat[(blockIdx.x % kStatWays) * kStatStride], t);
+    if (t) atomicAdd(a.costStat, t);
   }
   __syncthreads();
   const unsigned cap = a.groupCap;
@@ -900,8 +898,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         slot->cap = groups;
       }
       if (!slot->count) {
-        HIP_TRY(hipMallocAsync((void**)&slot->count, 8 * kCntStride * sizeof(unsigned), st));
-        HIP_TRY(hipMemsetAsync(slot->count, 0, 8 * kCntStride * sizeof(unsigned), st));
+        HIP_TRY(hipMallocAsync((void**)&slot->count, 8 * sizeof(unsigned), st));
+        HIP_TRY(hipMemsetAsync(slot->count, 0, 8 * sizeof(unsigned), st));
         slot->parity = 0;
       }
       if (ctx->orderFeedback && !(ctx->opts.flags & RTG_LAUNCH_NO_ORDER_FEEDBACK)) {
@@ -930,8 +928,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
             ce->cap = groups;
           }
           if (!ce->stat)
-            HIP_TRY(hipMallocAsync((void**)&ce->stat, 2 * kStatWords * sizeof(unsigned long long), st));
-          HIP_TRY(hipMemsetAsync(ce->stat, 0, 2 * kStatWords * sizeof(unsigned long long), st));
+            HIP_TRY(hipMallocAsync((void**)&ce->stat, 2 * sizeof(unsigned long long), st));
+          HIP_TRY(hipMemsetAsync(ce->stat, 0, 2 * sizeof(unsigned long long), st));
           ce->cur = 0;
           ce->key = key;
         }
@@ -940,11 +938,11 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         // it (and sums it into costStat) once a launch has written it, and
         // orders by it once a cull pass has summed it (costPrev)
         a.groupCost = ce->cost;
-        a.costStat = ce->launches >= 1 ? ce->stat + kStatWords * ce->cur : nullptr;
-        a.costPrev = ce->launches >= 2 ? ce->stat + kStatWords * (1 - ce->cur) : nullptr;
+        a.costStat = ce->launches >= 1 ? ce->stat + ce->cur : nullptr;
+        a.costPrev = ce->launches >= 2 ? ce->stat + (1 - ce->cur) : nullptr;
         if (ce->launches >= 1) ce->cur = 1 - ce->cur;
         // the next launch's costStat, zeroed by this launch's trace kernel
-        a.zeroStat = ce->stat + kStatWords * ce->cur;
+        a.zeroStat = ce->stat + ce->cur;
         ++ce->launches;
         costEntry = ce;
       }
@@ -957,8 +955,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       if (ctx->persistPerCU > 0) persist = (size_t)ctx->numCU * ctx->persistPerCU;
       a.groupList = slot->list;
       a.groupSel = slot->sel;
-      a.groupCount = slot->count + 4 * kCntStride * slot->parity;
-      a.zeroCount = slot->count + 4 * kCntStride * (1 - slot->parity);
+      a.groupCount = slot->count + 4 * slot->parity;
+      a.zeroCount = slot->count + 4 * (1 - slot->parity);
       slot->parity ^= 1u;
       a.groupCap = (unsigned)groups;  // light groups are listed from index groups - 1 down
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
@@ -1022,9 +1020,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       e = hipGetLastError();
     }
     if (e != hipSuccess) {  // no trace kernel zeroed the next launch's counters
-      (void)hipMemsetAsync(a.zeroCount, 0, 4 * kCntStride * sizeof(unsigned), st);
-      if (a.zeroStat)
-        (void)hipMemsetAsync(a.zeroStat, 0, kStatWords * sizeof(unsigned long long), st);
+      (void)hipMemsetAsync(a.zeroCount, 0, 4 * sizeof(unsigned), st);
+      if (a.zeroStat) (void)hipMemsetAsync(a.zeroStat, 0, sizeof(unsigned long long), st);
     }
     (void)hipEventRecord(slot->done, st);  // on every path
     if (costEntry) (void)hipEventRecord(costEntry->done, st);

@@ -514,19 +514,6 @@ struct DevScene {
   }
 };
 
-// Compacted launch counters (cull_groups_kernel): the four run lengths and
-// the launch-order feedback's cost sums.  RTG_CNT_SPREAD=1 (A/B builds) puts
-// each run length on its own 128-byte line and splits the cost sum into 8
-// partial sums on separate lines, so a cull pass's per-block atomics do not
-// all serialise on one line.
-#ifndef RTG_CNT_SPREAD
-#define RTG_CNT_SPREAD 0
-#endif
-constexpr unsigned kCntStride = RTG_CNT_SPREAD ? 32u : 1u;  // words between run lengths
-constexpr unsigned kStatWays = RTG_CNT_SPREAD ? 8u : 1u;    // partial cost sums
-constexpr unsigned kStatStride = RTG_CNT_SPREAD ? 16u : 1u; // u64 words between them
-constexpr unsigned kStatWords = kStatWays * kStatStride;    // one set of sums
-
 struct KernelArgs;
 typedef void (*TraceFn)(const KernelArgs);
 
@@ -1035,8 +1022,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
       const RTG_CONST KernelArgs* b = kargs();
       const RTG_CONST unsigned* gc = (const RTG_CONST unsigned*)b->groupCount;
       const unsigned cap = b->groupCap;
-      const unsigned e0 = gc[0], e1 = e0 + gc[kCntStride], e2 = e1 + gc[2 * kCntStride],
-                     e3 = e2 + gc[3 * kCntStride];
+      const unsigned e0 = gc[0], e1 = e0 + gc[1], e2 = e1 + gc[2], e3 = e2 + gc[3];
       return idx < e0 ? idx
            : idx < e1 ? cap - 1u - (idx - e0)
            : idx < e2 ? cap + (idx - e1)
@@ -1047,12 +1033,8 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
     if (gw == 0 && (threadIdx.x & 63u) == 0) {  // the next launch's counters (KernelArgs)
       const RTG_CONST KernelArgs* b = kargs();
       unsigned* zc = b->zeroCount;
-#pragma unroll
-      for (unsigned k = 0; k < 4; ++k) zc[k * kCntStride] = 0u;
-      if (unsigned long long* zs = b->zeroStat) {
-#pragma unroll
-        for (unsigned w = 0; w < kStatWays; ++w) zs[w * kStatStride] = 0ull;
-      }
+      zc[0] = zc[1] = zc[2] = zc[3] = 0u;
+      if (unsigned long long* zs = b->zeroStat) *zs = 0ull;
     }
     unsigned tg = t0;  // this group's start (the first one's includes the wave's set-up)
     for (unsigned idx = (unsigned)gw;; idx += kargs()->nPersist) {
