@@ -713,7 +713,7 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
                                 (ps.smask.size() + ps.cone.size() + ps.capOff.size() +
                                  ps.ovOff.size() + ps.nbrOff.size()) *
                                     sizeof(unsigned));
-  ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / kBvhWords);
+  ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / (kBvhWords * kBvhCopies));
   return RTG_OK;
 }
 

@@ -760,6 +760,39 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     ps->bvhNodes.clear();
     return false;
   }
+  if (kBvhCopies == 8u) {  // RTG_BVH_OCT: node copy per direction octant (rtg_trace.h)
+    const std::vector<float> src = ps->bvhNodes;
+    const size_t nn = src.size() / kBvhWords;
+    ps->bvhNodes.assign(nn * 8 * kBvhWords, 0.f);
+    for (size_t nd = 0; nd < nn; ++nd) {
+      const float* in = &src[nd * kBvhWords];
+      for (unsigned oct = 0; oct < 8; ++oct) {
+        const double sg[3] = {(oct & 1u) ? -1.0 : 1.0, (oct & 2u) ? -1.0 : 1.0,
+                              (oct & 4u) ? -1.0 : 1.0};
+        int ord[4] = {0, 1, 2, 3};
+        double key[4];
+        for (int k = 0; k < 4; ++k) {
+          int ch;
+          memcpy(&ch, &in[24 + k], 4);
+          if (ch > 0) {  // child box: its centre along the octant's diagonal
+            key[k] = 0.0;
+            for (int q = 0; q < 3; ++q)
+              key[k] += sg[q] * 0.5 * ((double)in[6 * k + q] + (double)in[6 * k + 3 + q]);
+          } else {
+            key[k] = ch < 0 ? 1e300 : __builtin_inf();  // spheres, then empty slots
+          }
+        }
+        std::stable_sort(ord, ord + 4, [&](int a, int b) { return key[a] < key[b]; });
+        float* out = &ps->bvhNodes[(nd * 8 + oct) * kBvhWords];
+        for (int k = 0; k < 4; ++k) {
+          const int j = ord[k];
+          for (int q = 0; q < 6; ++q) out[6 * k + q] = in[6 * j + q];
+          out[24 + k] = in[24 + j];
+          out[28 + k] = in[28 + j];
+        }
+      }
+    }
+  }
   return true;
 }
 

@@ -1441,6 +1441,15 @@ RTG_HD float norm_up(float a) { return sqrt_hw(a) * (1.0f + 0x1p-20f); }
 //   ch[k]          > 0 child node, < 0 ~sphere index, 0 empty
 //   cr[k]          a sphere slot's containment radius^2 (r + 1e-6f)^2
 constexpr int kBvhWords = 32;
+// RTG_BVH_OCT=1 (A/B builds): every node is stored 8 times, once per
+// direction octant, with its child boxes in front-to-back order along that
+// octant's diagonal (build_bvh); a query reads the copy of its wave's first
+// lane's octant and pushes the passing children in that order, instead of
+// sorting them by entry parameter (no keys, no compare-exchanges).
+#ifndef RTG_BVH_OCT
+#define RTG_BVH_OCT 0
+#endif
+constexpr unsigned kBvhCopies = RTG_BVH_OCT ? 8u : 1u;
 // One record of a sphere list (sphere_lists, rtg_scene_pack.h).
 struct ListRec {
   V3 c;
@@ -1532,9 +1541,9 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2,
 template <class Scene, class Leaf>
 RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
-                        bool shadowQ = false) {
+                        bool shadowQ = false, unsigned oct = 0) {
   BvhRec r;
-  sc.bvh_rec(nd, r);
+  sc.bvh_rec(nd * kBvhCopies + oct, r);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_SALU)  // issue-cost probes (A/B builds)
   {
     unsigned pad;
@@ -1566,7 +1575,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     if (pass) sc.count(kUBvhPass, 1);
     if (sc.any(pass)) {
       pc[k] = x;
-      pk[k] = sc.first_lane(tn);
+      if (!RTG_BVH_OCT) pk[k] = sc.first_lane(tn);
     }
   };
   auto sphere_slot = [&](int k, int x) {
@@ -1604,7 +1613,26 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
       else sphere_slot(k, x);
     }
   }
+  if (RTG_BVH_OCT) {  // slots already front to back: the nearest next, the others pushed far first
+    int nxt = 0;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+      if (pc[k] > 0) {
+        if (nxt > 0) st.push(nxt);
+        nxt = pc[k];
+      }
+    }
+    return nxt;
+  }
   return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
+}
+
+// The direction octant of the wave's first lane (RTG_BVH_OCT's node copy).
+template <class Scene>
+RTG_HD unsigned query_octant(const Scene& sc, const RayQ& q) {
+  if (!RTG_BVH_OCT) return 0u;
+  const V3 d = sc.first_lane(q.d);
+  return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
 }
 
 // Closest-hit and shadow updates for an accepted root (BVH and list loops),
@@ -1650,6 +1678,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
   const float dn = norm_up(q.den * 0.5f);
   const BoxQ b = make_boxq(q);
   BvhStack st(sc.bvh_stack());
+  const unsigned oct = query_octant(sc, q);
   unsigned nd = 0;  // the root
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
@@ -1660,7 +1689,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_closer(res, t, (int)i, minT, best);
-    });
+    }, false, oct);
     if (nx > 0) {
       nd = (unsigned)nx;
     } else {
@@ -1684,6 +1713,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
   const BoxQ b = make_boxq(q);
   sc.count(kCntBvhShadowQ, 1);
   BvhStack st(sc.bvh_stack());
+  const unsigned oct = query_octant(sc, q);
   unsigned nd = 0;  // the root
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
@@ -1694,7 +1724,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_blocker(res, t, q.d, gap, blk);
-    }, true);
+    }, true, oct);
     if (sc.all(blk)) break;
     if (nx > 0) {
       nd = (unsigned)nx;
@@ -1718,7 +1748,7 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
   for (;;) {        // wave-uniform
     sc.count(kUContBvhNode, 1);
     BvhRec r;
-    sc.bvh_rec(nd, r);
+    sc.bvh_rec(nd * kBvhCopies, r);
     int nxt = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

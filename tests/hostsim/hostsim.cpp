@@ -884,7 +884,7 @@ extern "C" void hostsim_list_records(const rtg_sphere* spheres, unsigned n,
   rtg::PackedScene ps;
   out[0] = out[1] = out[2] = 0;
   if (!rtg::build_bvh(spheres, n, &ps)) return;
-  out[2] = ps.bvhNodes.size() / rtg::kBvhWords;
+  out[2] = ps.bvhNodes.size() / (rtg::kBvhWords * rtg::kBvhCopies);
   rtg::sphere_lists(spheres, n, lights, m, &ps, (size_t)maxRecords);
   if (ps.capOff.empty()) return;
   out[0] = ps.capRec.size() / rtg::kListWords - 1;  // without the padding record
