@@ -1544,7 +1544,7 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
                         bool shadowQ = false, unsigned oct = 0) {
   BvhRec r;
-  sc.bvh_rec_q(nd * kBvhCopies + oct, r);
+  sc.bvh_rec(nd * kBvhCopies + oct, r);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_SALU)  // issue-cost probes (A/B builds)
   {
     unsigned pad;

@@ -23,9 +23,6 @@ namespace rtg {
 
 constexpr int kBlock = 256;
 
-#ifndef RTG_BVH_LOAD3  // A/B builds: DevScene::bvh_rec_q's three disjoint node loads
-#define RTG_BVH_LOAD3 0
-#endif
 #ifndef RTG_BVH_LOAD2  // A/B builds: DevScene::bvh_rec's paired node loads
 #define RTG_BVH_LOAD2 0
 #endif
@@ -347,33 +344,6 @@ struct DevScene {
       r.ch[k] = __float_as_int(b[8 + k]);
       r.cr[k] = b[12 + k];
     }
-  }
-  // The words a ray query reads (slots and children, not the containment
-  // radii): with RTG_BVH_LOAD3 (A/B builds) a 64-, a 32- and a 16-byte load
-  // into disjoint registers, so no load waits for the one before it (the
-  // two 64-byte loads above overlap in registers once the radii are dead,
-  // and the compiler then waits for the first before issuing the second).
-  __device__ __forceinline__ void bvh_rec_q(unsigned nd, BvhRec& r) const {
-#if RTG_BVH_LOAD3
-    typedef float f16 __attribute__((ext_vector_type(16)));
-    typedef float f8 __attribute__((ext_vector_type(8)));
-    typedef int i4 __attribute__((ext_vector_type(4)));
-    const RTG_CONST float* p = fidx(bvhNodes, kBvhWords * nd);
-    const f16 a = *(const RTG_CONST f16*)p;
-    const f8 b = *(const RTG_CONST f8*)(p + 16);
-    const i4 c = *(const RTG_CONST i4*)(p + 24);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) r.s[k] = a[k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r.s[16 + k] = b[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      r.ch[k] = c[k];
-      r.cr[k] = 0.f;
-    }
-#else
-    bvh_rec(nd, r);
-#endif
   }
   // One lane's value for wave-uniform decisions (traversal order, cone cull).
   __device__ __forceinline__ float first_lane(float v) const {

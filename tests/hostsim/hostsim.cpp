@@ -91,7 +91,6 @@ struct HostScene {
     return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
   }
   int* bvh_stack() const { return nullptr; }
-  void bvh_rec_q(unsigned nd, rtg::BvhRec& r) const { bvh_rec(nd, r); }
   void bvh_rec(unsigned nd, rtg::BvhRec& r) const {
     const float* g = bvhNodes + (size_t)rtg::kBvhWords * nd;
     memcpy(r.s, g, 24 * 4);
