@@ -1491,12 +1491,6 @@ struct BvhRec {
 // structurizer's flow instructions per slot (RTG_NODE_SPLIT=0; C5 -3.1 %,
 // DESIGN.md §4 item 48).  The box tests take the node's entry reach either
 // way, so the order changes nothing.
-// RTG_SCREEN_FUSE=1 (A/B builds): a sphere slot's screen and `behind` test
-// evaluated for every lane and taken as one exec-mask region, instead of
-// `behind` in a region nested inside the screen's.
-#ifndef RTG_SCREEN_FUSE
-#define RTG_SCREEN_FUSE 0
-#endif
 #ifndef RTG_NODE_SPLIT
 #define RTG_NODE_SPLIT 1
 #endif
@@ -1595,14 +1589,9 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
     const float cs = p2 - g[3];
     const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-    if (RTG_SCREEN_FUSE) {  // one exec-mask region for the screen and `behind`
-      const bool go = active & !beyond(p2, g[5], reachD) & !(v < 0.f) &
-                      !behind(0.5f * q.den, xd, cs, g[3]);
-      if (go) leaf((unsigned)~x, c, g[4]);
-    } else if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
-               !behind(0.5f * q.den, xd, cs, g[3])) {
+    if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
+        !behind(0.5f * q.den, xd, cs, g[3]))
       leaf((unsigned)~x, c, g[4]);
-    }
   };
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -1654,11 +1643,12 @@ RTG_HD unsigned query_octant(const Scene& sc, const RayQ& q) {
 #ifndef RTG_SEL_UPD
 #define RTG_SEL_UPD 1
 #endif
-// RTG_RES_FREE=1 (A/B builds): the updates ignore `res`.  ray_sphere returns
+// The updates ignore `res` (RTG_RES_FREE=0: they test it): ray_sphere returns
 // exactly 10000 when it accepts no root, and minT <= 1000 and the shadow reach
-// 1000 are below that, so t < minT, t == minT and t < 1000 already imply res.
+// 1000 are below that, so t < minT, t == minT and t < 1000 already imply res,
+// and the root test's flag is dead code (C5 -0.5 %).
 #ifndef RTG_RES_FREE
-#define RTG_RES_FREE 0
+#define RTG_RES_FREE 1
 #endif
 RTG_HD void take_closer(bool res, float t, int i, float& minT, int& best) {
   if (RTG_RES_FREE) res = true;
