@@ -1552,6 +1552,12 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     for (int k = 0; k < RTG_PAD_BVH_SALU; ++k) asm volatile("s_mov_b32 %0, 7" : "=s"(pad));  // no SCC write
   }
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_NOP)
+  {
+#pragma unroll
+    for (int k = 0; k < RTG_PAD_BVH_NOP; ++k) asm volatile("s_nop 0");
+  }
+#endif
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_VALU)
   {
     float pad;
