@@ -616,6 +616,11 @@ inline void bvh_grow(const double c[3], double r, double pmax, double omax, floa
   }
 }
 
+// RTG_BVH_OCT_KEY=1 (A/B builds): the octant copies order child boxes by
+// their near corner along the diagonal instead of their centre.
+#ifndef RTG_BVH_OCT_KEY
+#define RTG_BVH_OCT_KEY 0
+#endif
 inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
   ps->bvhNodes.clear();
   if (n <= kMaskMaxSpheres) return false;
@@ -774,10 +779,12 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
         for (int k = 0; k < 4; ++k) {
           int ch;
           memcpy(&ch, &in[24 + k], 4);
-          if (ch > 0) {  // child box: its centre along the octant's diagonal
+          if (ch > 0) {  // child box: its centre (or near corner) along the octant's diagonal
             key[k] = 0.0;
-            for (int q = 0; q < 3; ++q)
-              key[k] += sg[q] * 0.5 * ((double)in[6 * k + q] + (double)in[6 * k + 3 + q]);
+            for (int q = 0; q < 3; ++q) {
+              const double lo = in[6 * k + q], hi = in[6 * k + 3 + q];
+              key[k] += RTG_BVH_OCT_KEY ? sg[q] * (sg[q] > 0 ? lo : hi) : sg[q] * 0.5 * (lo + hi);
+            }
           } else {
             key[k] = ch < 0 ? 1e300 : __builtin_inf();  // spheres, then empty slots
           }
