@@ -1491,6 +1491,14 @@ struct BvhRec {
 // structurizer's flow instructions per slot (RTG_NODE_SPLIT=0; C5 -3.1 %,
 // DESIGN.md §4 item 48).  The box tests take the node's entry reach either
 // way, so the order changes nothing.
+// RTG_REACH_LIVE=1 (A/B builds): a node's box slots, tested after its sphere
+// slots (RTG_NODE_SPLIT), take the closest query's reach (minT) and the
+// shadow query's blocked lanes as those slots left them, not as they were
+// when the visit began: still conservative (later visits use them anyway),
+// and a leaf hit in the node can cull its sibling boxes.
+#ifndef RTG_REACH_LIVE
+#define RTG_REACH_LIVE 0
+#endif
 #ifndef RTG_NODE_SPLIT
 #define RTG_NODE_SPLIT 1
 #endif
@@ -1542,7 +1550,8 @@ RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2,
 template <class Scene, class Leaf>
 RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
-                        bool shadowQ = false, unsigned oct = 0) {
+                        bool shadowQ = false, unsigned oct = 0,
+                        const float* liveReach = nullptr, const bool* liveBlk = nullptr) {
   BvhRec r;
   sc.bvh_rec(nd * kBvhCopies + oct, r);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_SALU)  // issue-cost probes (A/B builds)
@@ -1577,8 +1586,10 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     sc.count(kUBvhSlot, 1);
     sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
     float tn;
-    const bool pass = active && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]),
-                                          reachT, tn);
+    // RTG_REACH_LIVE: the reach and activity after this node's sphere slots
+    const float rT = (RTG_REACH_LIVE && liveReach) ? *liveReach : reachT;
+    const bool act = (RTG_REACH_LIVE && liveBlk) ? (active && !*liveBlk) : active;
+    const bool pass = act && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]), rT, tn);
     if (pass) sc.count(kUBvhPass, 1);
     if (sc.any(pass)) {
       pc[k] = x;
@@ -1705,7 +1716,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_closer(res, t, (int)i, minT, best);
-    }, false, oct);
+    }, false, oct, &minT);
     if (nx > 0) {
       nd = (unsigned)nx;
     } else {
@@ -1740,7 +1751,7 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_blocker(res, t, q.d, gap, blk);
-    }, true, oct);
+    }, true, oct, nullptr, &blk);
     if (sc.all(blk)) break;
     if (nx > 0) {
       nd = (unsigned)nx;
