@@ -616,10 +616,10 @@ inline void bvh_grow(const double c[3], double r, double pmax, double omax, floa
   }
 }
 
-// RTG_BVH_OCT_KEY=1 (A/B builds): the octant copies order child boxes by
-// their near corner along the diagonal instead of their centre.
+// The octant copies order child boxes by their near corner along the
+// diagonal (RTG_BVH_OCT_KEY=0: by their centre).
 #ifndef RTG_BVH_OCT_KEY
-#define RTG_BVH_OCT_KEY 0
+#define RTG_BVH_OCT_KEY 1
 #endif
 inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
   ps->bvhNodes.clear();

@@ -1491,13 +1491,14 @@ struct BvhRec {
 // structurizer's flow instructions per slot (RTG_NODE_SPLIT=0; C5 -3.1 %,
 // DESIGN.md §4 item 48).  The box tests take the node's entry reach either
 // way, so the order changes nothing.
-// RTG_REACH_LIVE=1 (A/B builds): a node's box slots, tested after its sphere
-// slots (RTG_NODE_SPLIT), take the closest query's reach (minT) and the
-// shadow query's blocked lanes as those slots left them, not as they were
-// when the visit began: still conservative (later visits use them anyway),
-// and a leaf hit in the node can cull its sibling boxes.
+// A node's box slots, tested after its sphere slots (RTG_NODE_SPLIT), take
+// the closest query's reach (minT) and the shadow query's blocked lanes as
+// those slots left them, not as they were when the visit began: still
+// conservative (later visits use them anyway), and a leaf hit in the node
+// can cull its sibling boxes (RTG_REACH_LIVE=0: the visit's entry values;
+// DESIGN.md §4 item 51).
 #ifndef RTG_REACH_LIVE
-#define RTG_REACH_LIVE 0
+#define RTG_REACH_LIVE 1
 #endif
 #ifndef RTG_NODE_SPLIT
 #define RTG_NODE_SPLIT 1
