@@ -776,20 +776,25 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
                               (oct & 4u) ? -1.0 : 1.0};
         int ord[4] = {0, 1, 2, 3};
         double key[4];
+        int cls[4];  // 0 child box, 1 sphere, 2 empty
         for (int k = 0; k < 4; ++k) {
           int ch;
           memcpy(&ch, &in[24 + k], 4);
+          key[k] = 0.0;
+          cls[k] = ch > 0 ? 0 : ch < 0 ? 1 : 2;
           if (ch > 0) {  // child box: its centre (or near corner) along the octant's diagonal
-            key[k] = 0.0;
             for (int q = 0; q < 3; ++q) {
               const double lo = in[6 * k + q], hi = in[6 * k + 3 + q];
               key[k] += RTG_BVH_OCT_KEY ? sg[q] * (sg[q] > 0 ? lo : hi) : sg[q] * 0.5 * (lo + hi);
             }
-          } else {
-            key[k] = ch < 0 ? 1e300 : __builtin_inf();  // spheres, then empty slots
+          } else if (ch < 0 && RTG_LEAF_LIVE) {  // sphere: its near point along the diagonal
+            for (int q = 0; q < 3; ++q) key[k] += sg[q] * (double)in[6 * k + q];
+            key[k] = key[k] * 0.5773502691896258 - (double)in[6 * k + 5];
           }
         }
-        std::stable_sort(ord, ord + 4, [&](int a, int b) { return key[a] < key[b]; });
+        std::stable_sort(ord, ord + 4, [&](int a, int b) {
+          return cls[a] != cls[b] ? cls[a] < cls[b] : key[a] < key[b];
+        });
         float* out = &ps->bvhNodes[(nd * 8 + oct) * kBvhWords];
         for (int k = 0; k < 4; ++k) {
           const int j = ord[k];

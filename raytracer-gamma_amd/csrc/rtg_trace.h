@@ -1500,6 +1500,12 @@ struct BvhRec {
 #ifndef RTG_REACH_LIVE
 #define RTG_REACH_LIVE 1
 #endif
+// RTG_LEAF_LIVE=1 (A/B builds): the same for a node's sphere slots among
+// themselves (the distance prune takes the current minT, a blocked lane skips
+// the rest), with the octant copies' sphere slots ordered front to back.
+#ifndef RTG_LEAF_LIVE
+#define RTG_LEAF_LIVE 0
+#endif
 #ifndef RTG_NODE_SPLIT
 #define RTG_NODE_SPLIT 1
 #endif
@@ -1552,7 +1558,8 @@ template <class Scene, class Leaf>
 RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
                         bool shadowQ = false, unsigned oct = 0,
-                        const float* liveReach = nullptr, const bool* liveBlk = nullptr) {
+                        const float* liveReach = nullptr, const bool* liveBlk = nullptr,
+                        float liveDn = 0.f) {
   BvhRec r;
   sc.bvh_rec(nd * kBvhCopies + oct, r);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_SALU)  // issue-cost probes (A/B builds)
@@ -1607,8 +1614,10 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
     const float cs = p2 - g[3];
     const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-    if (active && !beyond(p2, g[5], reachD) && !(v < 0.f) &&
-        !behind(0.5f * q.den, xd, cs, g[3]))
+    // RTG_LEAF_LIVE: the reach and activity the node's earlier sphere slots left
+    const float rD = (RTG_LEAF_LIVE && liveReach) ? *liveReach * liveDn : reachD;
+    const bool act = (RTG_LEAF_LIVE && liveBlk) ? (active && !*liveBlk) : active;
+    if (act && !beyond(p2, g[5], rD) && !(v < 0.f) && !behind(0.5f * q.den, xd, cs, g[3]))
       leaf((unsigned)~x, c, g[4]);
   };
 #pragma unroll
@@ -1717,7 +1726,7 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
       bool res;
       const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
       take_closer(res, t, (int)i, minT, best);
-    }, false, oct, &minT);
+    }, false, oct, &minT, nullptr, dn);
     if (nx > 0) {
       nd = (unsigned)nx;
     } else {
