@@ -842,11 +842,7 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
     gf[3] = gs[3];
     gf[4] = g[3];
     gf[5] = ps->crad2[n + i];
-    // word 6: the distance prune radius of the masked scenes' fused closest
-    // loop (RTG_MASK_PRUNE, rtg_trace.h closest_sel_fused), as a BVH slot's
-    gf[6] = RTG_MASK_PRUNE ? round_up_f(fabs((double)s.radius) * (1.0 + 0x1p-7) * (1.0 + 0x1p-20))
-                           : 0.f;
-    gf[7] = 0.f;
+    gf[6] = 0.f; gf[7] = 0.f;
     prim_consts(s, &ps->prim[(size_t)i * 4]);
     float* mt = &ps->mats[(size_t)i * 8];
     mt[0] = s.material.matteColour.x; mt[1] = s.material.matteColour.y;

@@ -2264,30 +2264,17 @@ RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, boo
 // in index order, so the answer is closest_hit_mask's.
 // Fused form (sc.fuse & kFuseCone): screen and exact test in one wave-uniform
 // loop in index order (strict <, so the first index still wins ties).
-// RTG_MASK_PRUNE=1 (A/B builds): a sphere whose accepted roots all lie beyond
-// the current minT (`beyond`, the BVH slots' distance prune, with the
-// record's prune radius) skips its exact test: under the strict < such a
-// root cannot win.
-#ifndef RTG_MASK_PRUNE
-#define RTG_MASK_PRUNE 0
-#endif
 template <bool kFast, class Scene>
 RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
   float minT = 1000.f;
   int best = -1;
-  const float dn = RTG_MASK_PRUNE ? norm_up(q.den * 0.5f) : 0.f;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
     m &= ~(1ull << i);  // s_bitset0
     sc.count(kUSelIter, 1);
-    float rs, r2, ocu, rp;
-    const V3 c = sc.sphere_fused_rp(i, rs, r2, ocu, rp);
-    bool far = false;
-    if (RTG_MASK_PRUNE) {
-      const V3 p = vsub(q.o, c);
-      far = beyond(fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z)), rp, minT * dn);
-    }
-    if (!far && !(pass1_rad(q, c, rs) < 0.f)) {
+    float rs, r2, ocu;
+    const V3 c = sc.sphere_fused(i, rs, r2, ocu);
+    if (!(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntFullCand, 1);
       sc.count(kUSelExact, 1);
       bool res;

@@ -233,16 +233,6 @@ struct DevScene {
     oc = g[5];
     return v3(g[0], g[1], g[2]);
   }
-  __device__ __forceinline__ V3 sphere_fused_rp(unsigned i, float& rs, float& r2, float& oc,
-                                                float& rp) const {
-    typedef float f8 __attribute__((ext_vector_type(8)));
-    const f8 g = *(const RTG_CONST f8*)fidx(geom, 12 * (n4 + 4) + 8 * i);  // one load
-    rs = g[3];
-    r2 = g[4];
-    oc = g[5];
-    rp = g[6];
-    return v3(g[0], g[1], g[2]);
-  }
   __device__ __forceinline__ V3 sphere_contain(unsigned i, float& cr) const {
     return sphere(2 * (n4 + 4) + i, cr);
   }

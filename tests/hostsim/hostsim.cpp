@@ -106,10 +106,6 @@ struct HostScene {
   }
   rtg::V3 sphere_lane(unsigned i, float& r2) const { return sphere(i, r2); }
   float sphere_r2(unsigned i) const { return geom[4 * i + 3]; }
-  rtg::V3 sphere_fused_rp(unsigned i, float& rs, float& r2, float& oc, float& rp) const {
-    rp = geom[12 * (n4 + 4) + 8 * i + 6];
-    return sphere_fused(i, rs, r2, oc);
-  }
   rtg::V3 sphere_fused(unsigned i, float& rs, float& r2, float& oc) const {
     const float* g = geom + 12 * (n4 + 4) + 8 * i;
     rs = g[3];
