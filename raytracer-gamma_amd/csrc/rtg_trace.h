@@ -1657,24 +1657,9 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
 }
 
 // The direction octant of the wave's first lane (RTG_BVH_OCT's node copy).
-// RTG_OCT_MAJ=1 (A/B builds): the octant of the majority of the wave's lanes
-// per axis (three ballots) instead of the first lane's.
-#ifndef RTG_OCT_MAJ
-#define RTG_OCT_MAJ 0
-#endif
 template <class Scene>
 RTG_HD unsigned query_octant(const Scene& sc, const RayQ& q) {
   if (!RTG_BVH_OCT) return 0u;
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (RTG_OCT_MAJ) {
-    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
-    const unsigned half = (unsigned)__builtin_popcountll(act);
-    auto neg = [&](float v) {
-      return 2u * (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(v < 0.f)) > half;
-    };
-    return (neg(q.d.x) ? 1u : 0u) | (neg(q.d.y) ? 2u : 0u) | (neg(q.d.z) ? 4u : 0u);
-  }
-#endif
   const V3 d = sc.first_lane(q.d);
   return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
 }
