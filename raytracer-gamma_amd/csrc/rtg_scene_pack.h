@@ -700,22 +700,12 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     return lo + bestK;
   };
   int maxDepth = 0;
-  std::vector<double> nodeBox;  // per node: the union of its spheres' grown boxes
   // node for idx[lo, hi), returns its index
   std::function<int(unsigned, unsigned, int)> build = [&](unsigned lo, unsigned hi,
                                                           int depth) -> int {
     maxDepth = depth > maxDepth ? depth : maxDepth;
     const int node = (int)(ps->bvhNodes.size() / kBvhWords);
     ps->bvhNodes.resize(ps->bvhNodes.size() + kBvhWords, 0.f);
-    nodeBox.resize((size_t)(node + 1) * 6);
-    {
-      double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
-      for (unsigned t = lo; t < hi; ++t) grow(idx[t], mn, mx);
-      for (int q = 0; q < 3; ++q) {
-        nodeBox[(size_t)node * 6 + q] = mn[q];
-        nodeBox[(size_t)node * 6 + 3 + q] = mx[q];
-      }
-    }
     {  // empty slots: NaN geometry, child 0
       float* e = &ps->bvhNodes[(size_t)node * kBvhWords];
       for (int k = 0; k < 24; ++k) e[k] = __builtin_nanf("");
@@ -775,10 +765,10 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     ps->bvhNodes.clear();
     return false;
   }
-  if (kBvhCopies >= 8u) {  // RTG_BVH_OCT: node copy per direction octant (rtg_trace.h)
+  if (kBvhCopies == 8u) {  // RTG_BVH_OCT: node copy per direction octant (rtg_trace.h)
     const std::vector<float> src = ps->bvhNodes;
     const size_t nn = src.size() / kBvhWords;
-    ps->bvhNodes.assign(nn * kBvhCopies * kBvhWords, 0.f);
+    ps->bvhNodes.assign(nn * 8 * kBvhWords, 0.f);
     for (size_t nd = 0; nd < nn; ++nd) {
       const float* in = &src[nd * kBvhWords];
       for (unsigned oct = 0; oct < 8; ++oct) {
@@ -805,28 +795,14 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
         std::stable_sort(ord, ord + 4, [&](int a, int b) {
           return cls[a] != cls[b] ? cls[a] < cls[b] : key[a] < key[b];
         });
-        float* out = &ps->bvhNodes[(nd * kBvhCopies + oct) * kBvhWords];
+        float* out = &ps->bvhNodes[(nd * 8 + oct) * kBvhWords];
         for (int k = 0; k < 4; ++k) {
           const int j = ord[k];
           for (int q = 0; q < 6; ++q) out[6 * k + q] = in[6 * j + q];
           out[24 + k] = in[24 + j];
           out[28 + k] = in[28 + j];
         }
-        if (kBvhCopies == 9u) {  // RTG_NODE_SKIP: the node's bounding sphere {c, R}
-          const double* bx = &nodeBox[nd * 6];
-          float c[3];
-          double r2 = 0.0;
-          for (int q = 0; q < 3; ++q) c[q] = (float)(0.5 * (bx[q] + bx[3 + q]));
-          for (int q = 0; q < 3; ++q) {
-            const double e = fmax(fabs(bx[q] - c[q]), fabs(bx[3 + q] - c[q]));
-            r2 += e * e;
-          }
-          for (int q = 0; q < 3; ++q) out[28 + q] = c[q];
-          out[31] = round_up_f(sqrt(r2) * (1.0 + 0x1p-20));
-        }
       }
-      if (kBvhCopies == 9u)  // copy 8: the record as built (container_bvh's radii)
-        for (int w = 0; w < kBvhWords; ++w) ps->bvhNodes[(nd * 9 + 8) * kBvhWords + w] = in[w];
     }
   }
   return true;

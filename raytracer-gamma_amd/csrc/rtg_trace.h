@@ -1450,17 +1450,7 @@ constexpr int kBvhWords = 32;
 #ifndef RTG_BVH_OCT
 #define RTG_BVH_OCT 1
 #endif
-// RTG_NODE_SKIP=1 (A/B builds, with RTG_BVH_OCT): the octant copies carry
-// the node's own bounding sphere in their containment-radius words (a ninth
-// copy keeps the radii for container_bvh), and a visit whose lanes all have
-// that sphere beyond their current reach (`beyond`) skips the node's slots:
-// every accepted root in the subtree lies in the union of its grown boxes,
-// inside that sphere, so none is within reach.
-#ifndef RTG_NODE_SKIP
-#define RTG_NODE_SKIP 0
-#endif
-constexpr unsigned kBvhCopies = RTG_BVH_OCT ? (RTG_NODE_SKIP ? 9u : 8u) : 1u;
-constexpr unsigned kBvhContainCopy = RTG_BVH_OCT && RTG_NODE_SKIP ? 8u : 0u;
+constexpr unsigned kBvhCopies = RTG_BVH_OCT ? 8u : 1u;
 // One record of a sphere list (sphere_lists, rtg_scene_pack.h).
 struct ListRec {
   V3 c;
@@ -1593,13 +1583,6 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     for (int k = 0; k < RTG_PAD_BVH_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, 2.0" : "=v"(pad));
   }
 #endif
-  if (RTG_NODE_SKIP && RTG_BVH_OCT) {  // the node's sphere {c, R} in words 28-31
-    const V3 p = vsub(q.o, v3(r.cr[0], r.cr[1], r.cr[2]));
-    const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
-    const float rD = (liveReach != nullptr) ? *liveReach * liveDn : reachD;
-    const bool act = (liveBlk != nullptr) ? (active && !*liveBlk) : active;
-    if (sc.all(!act || beyond(p2, r.cr[3], rD))) return 0;
-  }
   int pc[4];
   float pk[4];
   float keyMax;  // bit pattern 0xFFFFFFFF: an invalid child sorts last (push_sorted)
@@ -1803,7 +1786,7 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
   for (;;) {        // wave-uniform
     sc.count(kUContBvhNode, 1);
     BvhRec r;
-    sc.bvh_rec(nd * kBvhCopies + kBvhContainCopy, r);
+    sc.bvh_rec(nd * kBvhCopies, r);
     int nxt = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
