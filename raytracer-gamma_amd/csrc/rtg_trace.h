@@ -332,25 +332,6 @@ struct Frame {
 #ifndef RTG_SCRATCH_NT
 #define RTG_SCRATCH_NT 0
 #endif
-// The reference's acceptance of the two roots (raytracer.h:120-137), sm
-// starting at 10000 and res false: the smallest root in (1e-5, 10000).
-// RTG_ACCEPT_MIN=1 (A/B builds): as a min, (u > 1e-5) ? min(u, sm) : sm
-// (a root >= sm leaves sm, NaN fails the first test), res = sm < 10000 -- the
-// same bits, with no mask combination in scalar registers.
-#ifndef RTG_ACCEPT_MIN
-#define RTG_ACCEPT_MIN 0
-#endif
-RTG_HD void accept_roots(float u0, float u1, float& sm, bool& res) {
-#if RTG_ACCEPT_MIN
-  sm = (u0 > 1.0e-5f) ? fminf(u0, sm) : sm;
-  sm = (u1 > 1.0e-5f) ? fminf(u1, sm) : sm;
-  res = sm < 10000.f;
-#else
-  if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
-  if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
-#endif
-}
-
 struct RayQ {
   V3 o, d;
   float a4, den, y;
@@ -463,7 +444,8 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
     const float u0 = quot(-b + root, q);
     const float u1 = quot(-b - root, q);
 #endif
-    accept_roots(u0, u1, sm, res);
+    if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+    if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
   }
   return sm;
 }
@@ -514,7 +496,8 @@ RTG_HD float ray_sphere_k(const RayQ& q, V3 c, float r2, bool& res) {
     const float root = rtg_sqrtf(radicand);
     const float u0 = quot_k<kFast>(-b + root, q);
     const float u1 = quot_k<kFast>(-b - root, q);
-    accept_roots(u0, u1, sm, res);
+    if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+    if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
   }
   return sm;
 }
@@ -1216,7 +1199,8 @@ RTG_HD int closest_hit4(const Scene& sc, V3 o, V3 d, float& tOut) {
         const float u1 = quot(-b[k] - root, q);
         float sm = 10000.f;
         bool res = false;
-        accept_roots(u0, u1, sm, res);
+        if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+        if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
         if (res && sm < minT) { minT = sm; best = (int)(i + k); }
       }
     }
@@ -2360,7 +2344,8 @@ RTG_HD int closest_hit_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, f
       const float u1 = quot_k<kFast>(bp - root, q);
       float sm = 10000.f;
       bool res = false;
-      accept_roots(u0, u1, sm, res);
+      if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
+      if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
       if (res && sm < minT) { minT = sm; best = (int)i; }
     }
   }
