@@ -599,8 +599,10 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   // Table limits of the kernel: a frame record keeps the refractive material
   // index in 22 bits (FrameC::meta, rm << 10), and scene tables are addressed
   // with 32-bit byte offsets (fidx / uidx).  For n < RTG_MAX_SPHERES the
-  // per-sphere tables end below 2^32 bytes (the fused records at 80 n bytes,
-  // the BVH at < 128 n); the sphere lists, which grow as O(m n^2), are capped
+  // per-sphere tables end below 2^32 bytes (the fused records at 80 n bytes);
+  // the BVH's octant copies take about 1 KB per node (~3/4 n nodes), and
+  // build_bvh refuses a tree past 2^32 bytes (the scene then takes the flat
+  // queries); the sphere lists, which grow as O(m n^2), are capped
   // separately (kListMaxRecords, sphere_lists: over it a scene has no lists
   // and its queries take the BVH).
   if (sphNum >= RTG_MAX_SPHERES) {
@@ -932,18 +934,22 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
           HIP_TRY(hipMemsetAsync(ce->stat, 0, 2 * sizeof(unsigned long long), st));
           ce->cur = 0;
           ce->key = key;
+        } else {
+          // launches of this entry on other streams may still add to or zero
+          // its sums: this stream waits for the last one (a no-op on its own)
+          HIP_TRY(hipStreamWaitEvent(st, ce->done, 0));
         }
-        ce->lastUse = ++ctx->costClock;
         // the trace kernel writes groupCost every launch; the cull pass reads
         // it (and sums it into costStat) once a launch has written it, and
-        // orders by it once a cull pass has summed it (costPrev)
+        // orders by it once a cull pass has summed it (costPrev).  The entry's
+        // own state (cur, launches) advances only once nothing can fail
+        // (commit below).
         a.groupCost = ce->cost;
         a.costStat = ce->launches >= 1 ? ce->stat + ce->cur : nullptr;
         a.costPrev = ce->launches >= 2 ? ce->stat + (1 - ce->cur) : nullptr;
-        if (ce->launches >= 1) ce->cur = 1 - ce->cur;
+        const unsigned nextCur = ce->launches >= 1 ? 1u - ce->cur : ce->cur;
         // the next launch's costStat, zeroed by this launch's trace kernel
-        a.zeroStat = ce->stat + ce->cur;
-        ++ce->launches;
+        a.zeroStat = ce->stat + nextCur;
         costEntry = ce;
       }
       cullGroups = groups;  // the cull pass is enqueued below, after the last failure point
@@ -956,8 +962,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       a.groupList = slot->list;
       a.groupSel = slot->sel;
       a.groupCount = slot->count + 4 * slot->parity;
-      a.zeroCount = slot->count + 4 * (1 - slot->parity);
-      slot->parity ^= 1u;
+      a.zeroCount = slot->count + 4 * (1 - slot->parity);  // parity flips at the commit
       a.groupCap = (unsigned)groups;  // light groups are listed from index groups - 1 down
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
       grid = dim3(a.nPersist, 1);
@@ -991,6 +996,16 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     }
     ctx->timelineCount = waves;
     a.timeline = ctx->timeline;
+  }
+  // Commit: nothing below fails before the launch, so the slot's counter set
+  // and the cost entry advance only now (an earlier error return leaves both
+  // as the previous launch left them: its trace kernel zeroed exactly the set
+  // this launch would have used).
+  if (slot) slot->parity ^= 1u;
+  if (costEntry) {
+    costEntry->lastUse = ++ctx->costClock;
+    if (costEntry->launches >= 1) costEntry->cur = 1 - costEntry->cur;
+    ++costEntry->launches;
   }
   // Stream work starts here, after every check and allocation that can fail,
   // so an error never leaves a cull pass (which zero-fills dst and fills the

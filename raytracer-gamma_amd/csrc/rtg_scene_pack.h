@@ -765,6 +765,13 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     ps->bvhNodes.clear();
     return false;
   }
+  // DevScene::bvh_rec addresses a node copy by a 32-bit byte offset
+  // (kBvhWords * 4 bytes per copy, kBvhCopies per node): a tree past 2^32
+  // bytes takes the flat queries instead (about 4 M nodes, n ~ 5 M spheres).
+  if ((double)(ps->bvhNodes.size() / kBvhWords) * kBvhCopies * kBvhWords * 4.0 >= 0x1p32) {
+    ps->bvhNodes.clear();
+    return false;
+  }
   if (kBvhCopies == 8u) {  // RTG_BVH_OCT: node copy per direction octant (rtg_trace.h)
     const std::vector<float> src = ps->bvhNodes;
     const size_t nn = src.size() / kBvhWords;

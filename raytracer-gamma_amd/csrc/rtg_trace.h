@@ -234,6 +234,8 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kUDiagContSame,  // (diagnostic) refraction target query, one hit sphere
              kULightDir,    // matte_light: a light no facing-away test excluded (direction)
              kUNbrIter,     // closest_near: one neighbour-list sphere (certificate, screen)
+             kUDiagInsig,     // (diagnostic) stage-0 query; lane value: intensity insignificant
+             kUDiagInsigAll,  // (diagnostic) stage-0 query whose every active lane is insignificant
              kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,
@@ -947,6 +949,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
     sc.count(kUNode, 1);
+    sc.count(kUDiagInsig, significant(I) ? 0 : 1);  // hit-or-miss would do (:455-460, :542-546)
+    if (sc.all(!significant(I))) sc.count(kUDiagInsigAll, 1);
     sc.probe_begin(kProbeClosest);
     int hit;
     if (usePrim) {  // the primary ray: only spheres its wave's bundle can reach
