@@ -661,6 +661,13 @@ def main():
                 if vi and work is not None:
                     roof["pmc_valu_insts"] = int(vi)
                     roof["model_vs_pmc_valu"] = round(work["valu_slots"] / vi, 3)
+                if vi:
+                    # the same roofline from the hardware's count of executed
+                    # VALU wave instructions (x 64 lanes) per launch, over this
+                    # run's mean kernel time: the model-free form of `frac`
+                    ach_pmc = vi * 64 / (kern_ms * 1e-3) / 1e12
+                    roof["achieved_pmc"] = round(ach_pmc, 3)
+                    roof["frac_pmc"] = round(ach_pmc / VALU_PEAK_TOPS, 4)
                 roof["traffic_note"] = ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
                                         f"({os.path.relpath(pmc, ROOT)})")
 

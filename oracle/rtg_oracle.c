@@ -212,8 +212,11 @@ static ORay calculateRefraction(const OSph* sph, unsigned n, const OIsect* is, O
   float sinA1 = 0.f;
   if (cosA1 <= -1.0) { cosA1 = -1.f; sinA1 = 0.f; }
   else if (cosA1 >= +1.f) { cosA1 = 1.f; sinA1 = 0.f; }
-  else if (cl) { sinA1 = sqrtf(1.f - (cosA1 * cosA1)); }          /* raytrace_kernel.cl:507 */
-  else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }  /* :683, f64 sqrt */
+  /* :683, f64 sqrt (1.0 is a double literal); raytrace_kernel.cl:507 has the
+   * same expression, and an OpenCL device with fp64 (gfx950) evaluates it in
+   * double too, so both modes share it (pinned: tests/test_gpu_parity.py
+   * test_opencl_reference_kernel_pins_oracle). */
+  else { sinA1 = (float)sqrt(1.0 - (double)(cosA1 * cosA1)); }
 
   const float kSmallShift = 0.01f;
   {
@@ -480,10 +483,16 @@ int oracle_render_rows(const void* spheres, unsigned n, const void* lights, unsi
 }
 
 /* The semantics of the reference's OpenCL kernel (raytrace_kernel.cl) under
- * IEEE binary32 arithmetic: f32 Fresnel (:399-432) and f32 sinA1 (:507), and
- * the return register zeroed by the reflection push (:835-845); the stack
- * capacity is the caller's (5 in the .cl, :58).  NOT pinned bit for bit: the
- * .cl ran under OpenCL's relaxed division/sqrt and FP contraction. */
+ * IEEE arithmetic with correctly rounded division and square root: f32
+ * Fresnel (:399-432), sinA1 in f64 as on the CPU path (:507, a double
+ * literal), and the return register zeroed by the reflection push
+ * (:835-845); the stack capacity is the caller's (5 in the .cl, :58).  Pinned
+ * bit for bit against the .cl itself, compiled for gfx950 with
+ * -cl-fp32-correctly-rounded-divide-sqrt -ffp-contract=off
+ * (oracle/build_ref_cl.sh, tests/test_gpu_parity.py
+ * test_opencl_reference_kernel_pins_oracle).  The author's own image of it,
+ * testPPM.ppm, used OpenCL's relaxed division/sqrt and contraction and is not
+ * reproducible bit for bit. */
 int oracle_render_rows_cl(const void* spheres, unsigned n, const void* lights, unsigned m,
                           unsigned W, unsigned H, float zoom, float aliasFactor, int stackSize,
                           const unsigned* rows, unsigned nrows, float* out, int nthreads) {

@@ -296,8 +296,6 @@ struct rtg_context {
   unsigned* capOff = nullptr;
   float* ovRec = nullptr;
   unsigned* ovOff = nullptr;
-  float* nbrRec = nullptr;    // neighbour lists of BVH scenes (null when none)
-  unsigned* nbrOff = nullptr;
   unsigned* maxScratch = nullptr;
   unsigned long long* diag = nullptr;  // probe counters of diagnostic variants
   unsigned long long* counts = nullptr;  // unit counters of the counting build (variant 120)
@@ -347,6 +345,7 @@ struct rtg_context {
   int persistPerCU = 0;  // > 0: fixed persistent waves per CU (RTG_PERSIST_PER_CU A/B knob)
   int lptMin = 2;        // heavy-first listing threshold (cull_groups_kernel; RTG_LPT_MIN A/B knob)
   size_t timelineCap = 0, timelineCount = 0;
+  size_t lastGroups = 0;  // pixel groups of the last compacted launch (rtg_diag_group_list)
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
   bool hasScene = false;
@@ -372,10 +371,6 @@ static void free_scene(rtg_context* c) {
   (void)hipFree(c->capOff);
   (void)hipFree(c->ovRec);
   (void)hipFree(c->ovOff);
-  (void)hipFree(c->nbrRec);
-  (void)hipFree(c->nbrOff);
-  c->nbrRec = nullptr;
-  c->nbrOff = nullptr;
   c->capRec = nullptr;
   c->capOff = nullptr;
   c->ovRec = nullptr;
@@ -562,6 +557,38 @@ int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* coun
   return RTG_OK;
 }
 
+int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
+                        unsigned long long* sel, unsigned* runs, size_t cap, size_t* groups) {
+  DeviceGuard deviceGuard;  // the caller's current device is restored on return
+  rtg_clear_error();
+  if (!ctx || !groups) return RTG_ERR_INVALID;
+  const rtg_context::GroupSlot& slot =
+      ctx->slots[(ctx->nextSlot + rtg_context::kSlots - 1) % rtg_context::kSlots];
+  if (!slot.count || !slot.list) {
+    rtg_set_error("rtg_diag_group_list: no compacted launch yet");
+    return RTG_ERR_INVALID;
+  }
+  const size_t ng = slot.cap;  // the slot's capacity; the last launch's group count
+  *groups = ctx->lastGroups;
+  const size_t k = cap < ctx->lastGroups ? cap : ctx->lastGroups;
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (cost) {
+    const rtg_context::CostEntry* ce = nullptr;
+    for (const auto& e : ctx->costs)
+      if (e.launches && e.cost && (!ce || e.lastUse > ce->lastUse)) ce = &e;
+    if (ce && ce->cap >= k) HIP_TRY(hipMemcpy(cost, ce->cost, k * sizeof(unsigned), hipMemcpyDeviceToHost));
+    else memset(cost, 0, k * sizeof(unsigned));
+  }
+  const size_t kl = 2 * k <= 2 * ng ? 2 * k : 2 * ng;
+  if (list) HIP_TRY(hipMemcpy(list, slot.list, kl * sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (sel) HIP_TRY(hipMemcpy(sel, slot.sel, kl * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  if (runs)  // the set the last launch used (its trace kernel zeroed the other one)
+    HIP_TRY(hipMemcpy(runs, slot.count + 4 * (1 - slot.parity), 4 * sizeof(unsigned),
+                      hipMemcpyDeviceToHost));
+  return RTG_OK;
+}
+
 int rtg_context_set_semantics(rtg_context* ctx, int semantics) {
   rtg_clear_error();
   if (!ctx || (semantics != RTG_SEMANTICS_CPU && semantics != RTG_SEMANTICS_OPENCL)) {
@@ -688,18 +715,6 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
     HIP_TRY(hipMemcpy(ctx->ovOff, ps.ovOff.data(), ps.ovOff.size() * sizeof(unsigned),
                       hipMemcpyHostToDevice));
   }
-  if (!ps.nbrOff.empty()) {
-    if (hipMalloc(&ctx->nbrRec, ps.nbrRec.size() * sizeof(float)) != hipSuccess ||
-        hipMalloc(&ctx->nbrOff, ps.nbrOff.size() * sizeof(unsigned)) != hipSuccess) {
-      free_scene(ctx);
-      rtg_set_error("hipMalloc failed for the neighbour lists");
-      return RTG_ERR_NOMEM;
-    }
-    HIP_TRY(hipMemcpy(ctx->nbrRec, ps.nbrRec.data(), ps.nbrRec.size() * sizeof(float),
-                      hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(ctx->nbrOff, ps.nbrOff.data(), ps.nbrOff.size() * sizeof(unsigned),
-                      hipMemcpyHostToDevice));
-  }
   ctx->n = sphNum;
   ctx->m = lgtNum;
   ctx->n4 = ps.n4;
@@ -710,10 +725,10 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
   ctx->sceneStats[1] = std::chrono::duration<double, std::milli>(tEnd - tUp).count();
   ctx->sceneStats[2] = (double)((ps.geom.size() + ps.crad2.size() + ps.mats.size() +
                                  ps.lights.size() + ps.prim.size() + ps.bvhNodes.size() +
-                                 ps.capRec.size() + ps.ovRec.size() + ps.nbrRec.size()) *
+                                 ps.capRec.size() + ps.ovRec.size()) *
                                     sizeof(float) +
                                 (ps.smask.size() + ps.cone.size() + ps.capOff.size() +
-                                 ps.ovOff.size() + ps.nbrOff.size()) *
+                                 ps.ovOff.size()) *
                                     sizeof(unsigned));
   ctx->sceneStats[3] = (double)(ps.bvhNodes.size() / (kBvhWords * kBvhCopies));
   return RTG_OK;
@@ -815,8 +830,6 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.capOff = ctx->capOff;
   a.ovRec = ctx->ovRec;
   a.ovOff = ctx->ovOff;
-  a.nbrRec = ctx->nbrRec;
-  a.nbrOff = ctx->nbrOff;
   a.n = ctx->n;
   a.m = ctx->m;
   a.n4 = ctx->n4;
@@ -964,6 +977,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       a.groupCount = slot->count + 4 * slot->parity;
       a.zeroCount = slot->count + 4 * (1 - slot->parity);  // parity flips at the commit
       a.groupCap = (unsigned)groups;  // light groups are listed from index groups - 1 down
+      ctx->lastGroups = groups;
       a.nPersist = (unsigned)(groups < persist ? groups : persist);
       grid = dim3(a.nPersist, 1);
     }

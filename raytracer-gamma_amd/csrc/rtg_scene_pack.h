@@ -59,11 +59,6 @@ struct PackedScene {
   // Sphere lists of BVH scenes (sphere_lists): capsule and overlap lists.
   std::vector<float> capRec, ovRec;
   std::vector<unsigned> capOff, ovOff;
-  // Neighbour lists of BVH scenes (neighbour_lists): per sphere h, the
-  // kNbrMax spheres nearest to h's origin ball by a certified lower bound
-  // on their hit distance, then a terminator record; nbrOff[h] = h's first.
-  std::vector<float> nbrRec;
-  std::vector<unsigned> nbrOff;
   unsigned n = 0, m = 0;
   unsigned n4 = 0;  // n rounded up to a multiple of 4; geom holds 3 x (n4 + 4) records + the fused part
 };
@@ -373,22 +368,6 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
   ps->ovRec.insert(ps->ovRec.end(), pad, pad + kListWords);
 }
 
-// Neighbour lists of BVH scenes (closest_near, rtg_trace.h).  A secondary
-// ray of sphere h (a refraction child that leaves h, or a reflection child)
-// starts in the origin ball B''_h = ball(c_h, rho_h) (cone_masks below: the
-// hit point passed h's guard test).  Every root t the reference accepts for
-// sphere i puts the exact point X = o + t d within r_i + mu_i of c_i,
-// mu_i = 2^-8 (|p_i| + r_i) with p_i = o - c_i (rtg_trace.h, "Why a box keeps
-// every sphere"), so the hit distance t |d| = |X - o| is at least
-//   delta_hi = D - rho_h - r_i - 2^-8 (D + rho_h + r_i)   (D = |c_i - c_h|)
-// minus a rounding slack, for every origin in B''_h.  h's list holds the
-// kNbrMax spheres of smallest delta_hi in increasing order (records {c, screen
-// r^2, r^2, delta (rounded down), index, refractive index}), then a
-// terminator {NaN centre, delta = R_h}: R_h is the smallest delta of the
-// spheres left out (+inf when none is).  A lane whose best root so far has
-// t |d| < delta of the next record is certified: no sphere after it can
-// reach t, so its lexicographic minimum of (t, index) is final; a lane the
-// terminator does not certify takes the BVH from its best.
 inline float round_up_f(double v) {
   float f = (float)v;
   if ((double)f < v) f = nextafterf(f, __builtin_inff());
@@ -399,63 +378,6 @@ inline float round_down_f(double v) {
   if ((double)f > v) f = nextafterf(f, -__builtin_inff());
   return f;
 }
-constexpr unsigned kNbrMax = 32;
-inline double origin_ball(const rtg_sphere& sh) {
-  const double ch = fabs((double)sh.pos.x) + fabs((double)sh.pos.y) + fabs((double)sh.pos.z);
-  const double g = guard_radius(sh);
-  return g + 0.0101 + 0x1p-20 * (ch + g);
-}
-inline void neighbour_lists(const rtg_sphere* spheres, unsigned n, PackedScene* ps,
-                            unsigned kmax = kNbrMax) {
-  ps->nbrRec.clear();
-  ps->nbrOff.clear();
-  if (!RTG_SEED_EXIT) return;  // closest_near is an A/B build (rtg_trace.h)
-  if (ps->capOff.empty() || n == 0) return;  // with the other lists only (finite scenes)
-  if ((double)n * n > kListMaxTests) return;  // O(n^2 log n) build
-  std::vector<std::pair<double, unsigned>> tmp(n);
-  ps->nbrRec.reserve((size_t)n * (std::min(kmax, n) + 1) * kListWords);
-  for (unsigned h = 0; h < n; ++h) {
-    const rtg_sphere& sh = spheres[h];
-    const double rho = origin_ball(sh);
-    const double chm = fmax(fabs((double)sh.pos.x), fmax(fabs((double)sh.pos.y),
-                                                         fabs((double)sh.pos.z)));
-    for (unsigned i = 0; i < n; ++i) {
-      const rtg_sphere& si = spheres[i];
-      const double dx = (double)si.pos.x - sh.pos.x, dy = (double)si.pos.y - sh.pos.y,
-                   dz = (double)si.pos.z - sh.pos.z;
-      const double D = sqrt(dx * dx + dy * dy + dz * dz);
-      const double ri = fabs((double)si.radius);
-      const double cim = fmax(fabs((double)si.pos.x), fmax(fabs((double)si.pos.y),
-                                                           fabs((double)si.pos.z)));
-      // the margin of the BVH boxes (bvh_grow): 2^-8 (|p| + r) + 2^-18 (|c| + r + |o|)
-      const double lb = D - rho - ri - 0x1p-8 * (D + rho + ri) -
-                        0x1p-18 * (cim + ri + chm + rho) - 0x1p-20;
-      tmp[i] = {i == h ? -1.0 : lb, i};
-    }
-    std::sort(tmp.begin(), tmp.end());
-    const unsigned k = std::min(kmax, n);
-    ps->nbrOff.push_back((unsigned)(ps->nbrRec.size() / kListWords));
-    for (unsigned q = 0; q < k; ++q) {
-      const unsigned i = tmp[q].second;
-      const rtg_sphere& si = spheres[i];
-      const float r2 = si.radius * si.radius;  // raytracer.h:100
-      unsigned idx = i;
-      float fi;
-      memcpy(&fi, &idx, 4);
-      const float w[kListWords] = {si.pos.x, si.pos.y, si.pos.z, screen_r2(r2), r2,
-                                   round_down_f(tmp[q].first), fi, si.material.refractiveIndex};
-      ps->nbrRec.insert(ps->nbrRec.end(), w, w + kListWords);
-    }
-    const float R = k < n ? round_down_f(tmp[k].first) : __builtin_inff();
-    const float term[kListWords] = {NAN, NAN, NAN, NAN, NAN, R, 0.f, 1.f};
-    ps->nbrRec.insert(ps->nbrRec.end(), term, term + kListWords);
-  }
-  ps->nbrOff.push_back((unsigned)(ps->nbrRec.size() / kListWords));
-  // a padding record: the kernel reads records in pairs
-  const float pad[kListWords] = {NAN, NAN, NAN, NAN, NAN, NAN, 0.f, 1.f};
-  ps->nbrRec.insert(ps->nbrRec.end(), pad, pad + kListWords);
-}
-
 // Secondary-ray cone masks.  A secondary ray of sphere h starts in the origin
 // ball B''_h = ball(c_h, rho_h), rho_h = g_h + 0.0101 + 2^-20 (|c_h| + g_h):
 // refraction children start at the hit point P (|P - c_h| <= g_h, the guard
@@ -616,11 +538,6 @@ inline void bvh_grow(const double c[3], double r, double pmax, double omax, floa
   }
 }
 
-// The octant copies order child boxes by their near corner along the
-// diagonal (RTG_BVH_OCT_KEY=0: by their centre).
-#ifndef RTG_BVH_OCT_KEY
-#define RTG_BVH_OCT_KEY 1
-#endif
 inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
   ps->bvhNodes.clear();
   if (n <= kMaskMaxSpheres) return false;
@@ -772,7 +689,7 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
     ps->bvhNodes.clear();
     return false;
   }
-  if (kBvhCopies == 8u) {  // RTG_BVH_OCT: node copy per direction octant (rtg_trace.h)
+  {  // a copy of every node per direction octant (rtg_trace.h kBvhCopies)
     const std::vector<float> src = ps->bvhNodes;
     const size_t nn = src.size() / kBvhWords;
     ps->bvhNodes.assign(nn * 8 * kBvhWords, 0.f);
@@ -789,12 +706,12 @@ inline bool build_bvh(const rtg_sphere* spheres, unsigned n, PackedScene* ps) {
           memcpy(&ch, &in[24 + k], 4);
           key[k] = 0.0;
           cls[k] = ch > 0 ? 0 : ch < 0 ? 1 : 2;
-          if (ch > 0) {  // child box: its centre (or near corner) along the octant's diagonal
+          if (ch > 0) {  // child box: its near corner along the octant's diagonal (item 51)
             for (int q = 0; q < 3; ++q) {
               const double lo = in[6 * k + q], hi = in[6 * k + 3 + q];
-              key[k] += RTG_BVH_OCT_KEY ? sg[q] * (sg[q] > 0 ? lo : hi) : sg[q] * 0.5 * (lo + hi);
+              key[k] += sg[q] * (sg[q] > 0 ? lo : hi);
             }
-          } else if (ch < 0 && RTG_LEAF_LIVE) {  // sphere: its near point along the diagonal
+          } else if (ch < 0) {  // sphere: its near point along the diagonal (item 52)
             for (int q = 0; q < 3; ++q) key[k] += sg[q] * (double)in[6 * k + q];
             key[k] = key[k] * 0.5773502691896258 - (double)in[6 * k + 5];
           }
@@ -863,7 +780,6 @@ inline void pack_scene(const rtg_sphere* spheres, unsigned n, const rtg_light* l
   else ps->cone.clear();
   if (build_bvh(spheres, n, ps)) {
     sphere_lists(spheres, n, lights, m, ps);
-    neighbour_lists(spheres, n, ps);
   }
   for (unsigned l = 0; l < m; ++l) {
     float* p = &ps->lights[(size_t)l * 6];

@@ -233,7 +233,6 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kUDiagEnterSame, // (diagnostic) ... the same sphere
              kUDiagContSame,  // (diagnostic) refraction target query, one hit sphere
              kULightDir,    // matte_light: a light no facing-away test excluded (direction)
-             kUNbrIter,     // closest_near: one neighbour-list sphere (certificate, screen)
              kUDiagInsig,     // (diagnostic) stage-0 query; lane value: intensity insignificant
              kUDiagInsigAll,  // (diagnostic) stage-0 query whose every active lane is insignificant
              kCntSlots };
@@ -260,28 +259,6 @@ struct FrameC {
                   // inside: the reflection child starts inside the origin sphere)
 };
 struct FrameR { V3 ro, rd, rI; };
-RTG_HD void frame_r_store(FrameR& dst, const FrameR& v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  float* d = &dst.ro.x;
-  const float* s = &v.ro.x;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) __builtin_nontemporal_store(s[k], d + k);
-#else
-  dst = v;
-#endif
-}
-RTG_HD FrameR frame_r_load(const FrameR& src) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  FrameR v;
-  float* d = &v.ro.x;
-  const float* s = &src.ro.x;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) d[k] = __builtin_nontemporal_load(s + k);
-  return v;
-#else
-  return src;
-#endif
-}
 
 // Local (private-memory) storage of the colour part, used when the scene does
 // not provide per-lane LDS frames.
@@ -313,27 +290,6 @@ struct Frame {
 // property over 1e9 operand pairs (incl. subnormal numerators and values at
 // both thresholds) for den in [2^-60, 2^60].  Outside that range the correctly
 // rounded division is used.
-#ifndef RTG_FR0_REGS  // A/B builds: level 0's reflection child ray in VGPRs
-#define RTG_FR0_REGS 0
-#endif
-// Probe builds only (RTG_SCRATCH_X2=1): every reflection child ray is also
-// written to a second private array and read back at unwind, doubling the
-// scratch traffic without changing any result — an A/B against the default
-// prices that traffic.
-#ifndef RTG_SCRATCH_X2
-#define RTG_SCRATCH_X2 0
-#endif
-// BVH scenes: refraction children that leave their sphere take
-// closest_near over the neighbour lists (1; an A/B build: measured in the
-// host build at about 1 % less executed work on C5).
-#ifndef RTG_SEED_EXIT
-#define RTG_SEED_EXIT 0
-#endif
-// A/B builds (RTG_SCRATCH_NT=1): the reflection child rays' scratch stores
-// and loads with the nontemporal cache policy (scratch traffic).
-#ifndef RTG_SCRATCH_NT
-#define RTG_SCRATCH_NT 0
-#endif
 struct RayQ {
   V3 o, d;
   float a4, den, y;
@@ -400,12 +356,9 @@ RTG_HD float quot_k(float x, const RayQ& q) {
 // mask): its wave then skips the square root and the quotients unless a
 // lane grazes it.  tests/test_oracle.py::
 // test_no_root_is_exact checks it against the reference's test.
-// Default (1): the masked scenes' shadow queries (C3 -0.9 %, C4 -1 %); the
-// BVH scenes' (2) cost the BVH kernel two VGPRs past 80, one wave per SIMD
-// less: C5 145.5 vs 130.1 ms.
-#ifndef RTG_NOROOT  // 0 off, 1 masked-scene shadow queries, 2 also BVH-scene shadow queries
-#define RTG_NOROOT 1
-#endif
+// Used by the masked scenes' shadow queries (C3 -0.9 %, C4 -1 %); in the
+// BVH scenes' it cost the BVH kernel two VGPRs past 80, one wave per SIMD
+// less: C5 145.5 vs 130.1 ms (DESIGN.md §4 item 41).
 #ifndef RTG_NOROOT_K  // the inside bound (tests probe larger ones)
 #define RTG_NOROOT_K 8e-6f
 #endif
@@ -417,10 +370,7 @@ RTG_HD bool no_root(const RayQ& q, float b, float cc) {
 // (1e-5, 10000) or 10000 when none (`res` tells).  kNone: lanes where
 // no_root holds skip the roots (same answer).
 // Both quotients' division fallback in one wave-uniform branch instead of
-// one each (same values; RTG_QUOT2=0: one each).
-#ifndef RTG_QUOT2
-#define RTG_QUOT2 1
-#endif
+// one each (same values).
 template <bool kNone = false>
 RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   V3 disp = vsub(q.o, c);
@@ -431,7 +381,6 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
   res = false;
   if (radicand >= 0.0f && !(kNone && no_root(q, b, cc))) {
     const float root = rtg_sqrtf(radicand);
-#if RTG_QUOT2
     const float x0 = -b + root, x1 = -b - root;
     float u0 = quot_k<true>(x0, q);
     float u1 = quot_k<true>(x1, q);
@@ -442,47 +391,17 @@ RTG_HD float ray_sphere(const RayQ& q, V3 c, float r2, bool& res) {
         u1 = x1 / q.den;
       }
     }
-#else
-    const float u0 = quot(-b + root, q);
-    const float u1 = quot(-b - root, q);
-#endif
     if (u0 > 1.0e-5f) { if (u0 < sm) { sm = u0; res = true; } }
     if (u1 > 1.0e-5f) { if (u1 < sm) { sm = u1; res = true; } }
   }
   return sm;
 }
 
-// The same test with selects in place of the divergent branches (for the
-// BVH scenes' leaf and list loops, whose waves are scalar-issue bound: each
-// divergent if costs an exec-mask save, a branch and a restore).  Lanes with
-// a negative radicand compute discarded roots; the square root's fallback
-// and the quotient's stay wave-uniform branches (RTG_SEL_EXACT=0: branches).
-#ifndef RTG_SEL_EXACT
-#define RTG_SEL_EXACT 0
-#endif
-RTG_HD float ray_sphere_sel(const RayQ& q, V3 c, float r2, bool& res) {
-  V3 disp = vsub(q.o, c);
-  const float b = 2.0f * vdot(q.d, disp);
-  const float cc = vdot(disp, disp) - r2;
-  const float radicand = (b * b) - (q.a4 * cc);
-  const bool ok = radicand >= 0.0f;
-  float root = sqrt_fast(radicand);  // (NaN for a negative radicand: not used)
-  if (any_lane(ok && !sqrt_fast_range(radicand))) {
-    no_speculate();
-    if (ok && !sqrt_fast_range(radicand)) root = sqrtf(radicand);
-  }
-  const float u0 = quot(-b + root, q);
-  const float u1 = quot(-b - root, q);
-  const bool a0 = ok && u0 > 1.0e-5f && u0 < 10000.f;
-  float sm = a0 ? u0 : 10000.f;
-  const bool a1 = ok && u1 > 1.0e-5f && u1 < sm;
-  sm = a1 ? u1 : sm;
-  res = a0 || a1;
-  return sm;
-}
+// The BVH leaves' and sphere lists' root test (a select form of it, branch-
+// free for lanes with a negative radicand, measured neutral on C5: DESIGN.md
+// §4 item 45).
 template <bool kNone = false>
 RTG_HD float ray_sphere_leaf(const RayQ& q, V3 c, float r2, bool& res) {
-  if (RTG_SEL_EXACT) return ray_sphere_sel(q, c, r2, res);
   return ray_sphere<kNone>(q, c, r2, res);
 }
 
@@ -832,7 +751,6 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   float sinA1 = 0.f;
   if (cosA1 <= -1.0f) { cosA1 = -1.f; sinA1 = 0.f; }
   else if (cosA1 >= 1.f) { cosA1 = 1.f; sinA1 = 0.f; }
-  else if (kCL) { sinA1 = rtg_sqrtf(1.f - (cosA1 * cosA1)); }  // raytrace_kernel.cl:507
   else {
     sc.probe_begin(kProbeSplitSin);
     sinA1 = (float)sqrt_d_unit(1.0 - (double)(cosA1 * cosA1));
@@ -914,42 +832,30 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
 // kCL: the reference OpenCL kernel's semantics (raytrace_kernel.cl:641-867):
-// f32 Fresnel and sinA1, and the return register zeroed by the reflection
-// push (:835-845), so a reflection child that leaves it stale returns 0 and a
-// leaf's colour is doubled once, not twice.
+// f32 Fresnel, and the return register zeroed by the reflection push
+// (:835-845), so a reflection child that leaves it stale returns 0 and a
+// leaf's colour is doubled once, not twice.  sinA1 stays f64: :507 is the CPU
+// path's double expression, which the .cl compiled for gfx950 evaluates in
+// double too (pinned against it, oracle/build_ref_cl.sh).
 template <int S, int Q, bool kCL = false, class Scene, class FStore>
 RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = false,
                        uint64_t primSel = ~0ull) {
   constexpr int NF = (S > 1) ? (S - 1) : 1;
   FrameR fr[NF];                        // reflection child rays (private memory)
-  FrameR fr0;                           // RTG_FR0_REGS: level 0's, in VGPRs
-#if RTG_SCRATCH_X2
-  FrameR frx[NF];                       // probe: a second copy (scratch traffic x2)
-#endif
   int sp = 0;                           // == level of the node being processed
   V3 ret = v3(0.f, 0.f, 0.f);           // colourSum register
   V3 o = v3(0.f, 0.f, 0.f), d = dir0, I = v3(1.f, 1.f, 1.f);
   int rm = (int)sc.n;                   // background material
   int enterH = -1;  // Q == 4: the sphere this ray entered (refraction child), or -1
   int originH = -1;  // Q == 4: the sphere whose origin ball holds this ray's origin, or -1
-  int exitH = -1;    // Q == 4, RTG_SEED_EXIT: the sphere this ray leaves (closest_seeded), or -1
-#if defined(__HIP_DEVICE_COMPILE__) && (defined(RTG_PAD_SALU) || defined(RTG_PAD_VALU))
-  unsigned padS;  // issue-cost probes (A/B builds only): dummy work per node
-  float padV;
-#endif
   for (;;) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_SALU)
-#pragma unroll
-    for (int k = 0; k < RTG_PAD_SALU; ++k) asm volatile("s_add_u32 %0, 7, 1" : "=s"(padS));
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_VALU)
-#pragma unroll
-    for (int k = 0; k < RTG_PAD_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, 2.0" : "=v"(padV));
-#endif
     // ---------------- stage 0 (raytracer.h:454-550) ----------------
     float t;
     sc.count(kUNode, 1);
-    sc.count(kUDiagInsig, significant(I) ? 0 : 1);  // hit-or-miss would do (:455-460, :542-546)
+    // insignificant intensity: hit or miss would do (:455-460, :542-546); a
+    // hit-or-miss BVH query for waves of only such rays measured neutral on
+    // C5 (13.6 % of its stage-0 waves)
+    sc.count(kUDiagInsig, significant(I) ? 0 : 1);
     if (sc.all(!significant(I))) sc.count(kUDiagInsigAll, 1);
     sc.probe_begin(kProbeClosest);
     int hit;
@@ -993,12 +899,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       sc.count(kUQuery, 1);
       hit = closest_enter_list(sc, make_query(o, d), sc.first_lane_i(enterH), t, ok);
       if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
-    } else if (RTG_SEED_EXIT && Q == 4 && sc.has_nbr() && sc.all(exitH >= 0) &&
-               sc.all(sc.first_lane_i(exitH) == exitH)) {
-      // BVH scene, coherent wave of rays from one sphere's origin ball: its
-      // neighbour list, then the BVH for the lanes it does not certify
-      sc.count(kUQuery, 1);
-      hit = closest_near(sc, make_query(o, d), sc.first_lane_i(exitH), t);
     } else {
       if (sc.has_bvh() && sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
       sc.count(kCntFullQ, 1);
@@ -1006,7 +906,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     }
     enterH = -1;
     originH = -1;
-    exitH = -1;
     sc.probe_end(kProbeClosest);
     sc.probe_begin(kProbeShade);
     if (hit < 0) {
@@ -1081,12 +980,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             r.rd = rd;
             r.ro = vadd(P, vsmul(0.01f, rd));
             r.rI = rc;
-            if (RTG_FR0_REGS && lv == 0) fr0 = r;
-            else if (RTG_SCRATCH_NT) frame_r_store(fr[lv], r);
-            else fr[lv] = r;
-#if RTG_SCRATCH_X2
-            frx[lv] = r;
-#endif
+            fr[lv] = r;
           }
           sc.count(kUDescend, 1);
           ++sp;
@@ -1094,7 +988,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           // refraction child: calculateRefraction's refracted ray (:805-809);
           // hit from outside (cosA1 < 0): the child starts in sphere `hit`
           if (Q == 4 && vdot(d, N) < 0.f) enterH = hit;
-          else if (RTG_SEED_EXIT && Q == 4 && guardOK) exitH = hit;  // leaves hit from P
           if (Q == 4 && guardOK && sc.has_cone()) originH = hit;  // the child starts at P
           I = vsmul((1.f - R), vsmul(tr, I));
           o = P;
@@ -1127,22 +1020,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
         fc.set(lv, f);
-        FrameR r;
-        if (RTG_FR0_REGS && lv == 0) {
-          r = fr0;
-        } else {
-#if defined(__HIP_DEVICE_COMPILE__)
-          if (RTG_FR0_REGS) asm volatile("" ::: "memory");  // no speculative scratch load
-#endif
-          r = RTG_SCRATCH_NT ? frame_r_load(fr[lv]) : fr[lv];
-        }
-#if RTG_SCRATCH_X2 && defined(__HIP_DEVICE_COMPILE__)
-        {
-          const FrameR rx = frx[lv];  // consumed by an empty asm: the load stays
-          asm volatile("" ::"v"(rx.ro.x), "v"(rx.ro.y), "v"(rx.ro.z), "v"(rx.rd.x), "v"(rx.rd.y),
-                       "v"(rx.rd.z), "v"(rx.rI.x), "v"(rx.rI.y), "v"(rx.rI.z));
-        }
-#endif
+        const FrameR r = fr[lv];
         o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 10);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if (Q == 4 && (f.meta & 0x200u)) enterH = originH;  // reflection back into it
@@ -1153,8 +1031,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       --sp;
     }
     sc.probe_end(kProbeUnwind);
-#if defined(__HIP_DEVICE_COMPILE__) && (defined(RTG_PAD_SALU) || defined(RTG_PAD_VALU))
-#endif
     if (!descend) return ret;
   }
 }
@@ -1284,13 +1160,10 @@ RTG_HD float pass1_rad(const RayQ& q, V3 c, float rs) {
 // own float test on adversarial rays.  Used by the BVH scenes' queries (BVH
 // leaves, sphere lists): C5 138.8-138.9 vs 139.3-139.4 ms without; the
 // masked scenes' fused loops leave it out (C3 1.485-1.496 ms without it,
-// 1.508-1.532 with).  RTG_BEHIND=0 (A/B builds) turns it off.
-#ifndef RTG_BEHIND
-#define RTG_BEHIND 1
-#endif
+// 1.508-1.532 with).
 RTG_HD bool behind(float a, float x, float cs, float rs) {
   const float pp = cs + rs;
-  return RTG_BEHIND && x > 0x1p-20f * (a + pp) && cs > 0x1p-18f * rs && x < 75.f * a &&
+  return x > 0x1p-20f * (a + pp) && cs > 0x1p-18f * rs && x < 75.f * a &&
          pp < 0x1p20f * a;
 }
 // pass1_rad's screen and `behind` in one: false when sphere (c, rs) can have
@@ -1446,15 +1319,12 @@ RTG_HD float norm_up(float a) { return sqrt_hw(a) * (1.0f + 0x1p-20f); }
 //   cr[k]          a sphere slot's containment radius^2 (r + 1e-6f)^2
 constexpr int kBvhWords = 32;
 // Every node is stored 8 times, once per direction octant, with its child
-// boxes in front-to-back order along that octant's diagonal (build_bvh); a
-// query reads the copy of its wave's first lane's octant and pushes the
-// passing children in that order instead of sorting them by entry parameter
-// (no keys, no compare-exchanges): C5 -0.6 %.
-// RTG_BVH_OCT=0: one copy, children sorted per visit (push_sorted).
-#ifndef RTG_BVH_OCT
-#define RTG_BVH_OCT 1
-#endif
-constexpr unsigned kBvhCopies = RTG_BVH_OCT ? 8u : 1u;
+// boxes in front-to-back order along that octant's diagonal by their near
+// corners, then its sphere slots front to back by their near points
+// (build_bvh); a query reads the copy of its wave's first lane's octant and
+// pushes the passing children in that order instead of sorting them by entry
+// parameter (no keys, no compare-exchanges): DESIGN.md §4 items 49, 51, 52.
+constexpr unsigned kBvhCopies = 8u;
 // One record of a sphere list (sphere_lists, rtg_scene_pack.h).
 struct ListRec {
   V3 c;
@@ -1467,98 +1337,25 @@ struct BvhRec {
   float cr[4];
 };
 
-// Children of a node for the wave: of the valid (child, key) pairs, keys =
-// a lane's box entry parameter (wave-uniform), the nearest is returned (the
-// next node: no stack round trip) and the others are pushed in slot order.
-// Three compare-exchanges bubble the nearest to the end.  The keys are
-// compared as unsigned bit patterns: an entry parameter is max(..., 0) >= 0
-// and never NaN (slab_pass), and for such floats the patterns order like the
-// values (a -0 would sort last; the order only decides which node is visited
-// first, never an answer), so the compare-exchanges are scalar integer work.
+// One node of a ray query: distance pruning + pass-1 screens of its sphere
+// slots (reach `reachD` in distance units), handed to `leaf(i, c, r2)` for
+// the lanes that pass, then box tests of its child slots (reach `reachT` in
+// ray parameter units); child nodes some active lane still needs come in the
+// octant copy's front-to-back order (the nearest returned, the others pushed
+// far first).  `active`: the lane still queries.  Returns the next node (> 0)
+// or 0.
 // The waves are scalar-issue bound (an extra scalar instruction per node
-// costs 2.4 times an extra vector one): a full
-// five-exchange sort visited 1 % fewer nodes and ran C5 4 % slower
-// (RTG_BVH_SORT=0, A/B builds).
-#ifndef RTG_BVH_SORT
-#define RTG_BVH_SORT 1
-#endif
-// List loops (blocked_cap, closest_enter_list, container_list): both records
-// of a pair, with one exit test per pair (1), instead of stopping at the
-// list's end and testing for an exit after each record (0).  C5 122.9-123.3
-// vs 124.9-125.1 ms; selects for the child-box take measured 1.2 % slower.
-#ifndef RTG_LIST_PAIR
-#define RTG_LIST_PAIR 1
-#endif
-// A node's sphere slots in one unrolled pass and its box slots in a second,
-// each slot behind one wave-uniform test of its child word, instead of one
-// pass that tests empty / box / sphere, whose if/else costs the
-// structurizer's flow instructions per slot (RTG_NODE_SPLIT=0; C5 -3.1 %,
-// DESIGN.md §4 item 48).  The box tests take the node's entry reach either
-// way, so the order changes nothing.
-// A node's box slots, tested after its sphere slots (RTG_NODE_SPLIT), take
-// the closest query's reach (minT) and the shadow query's blocked lanes as
-// those slots left them, not as they were when the visit began: still
-// conservative (later visits use them anyway), and a leaf hit in the node
-// can cull its sibling boxes (RTG_REACH_LIVE=0: the visit's entry values;
-// DESIGN.md §4 item 51).
-#ifndef RTG_REACH_LIVE
-#define RTG_REACH_LIVE 1
-#endif
-// The same for a node's sphere slots among themselves (the distance prune
-// takes the current minT, a blocked lane skips the rest), with the octant
-// copies' sphere slots ordered front to back (RTG_LEAF_LIVE=0: entry values,
-// slot order; C5 -0.6 %).
-#ifndef RTG_LEAF_LIVE
-#define RTG_LEAF_LIVE 1
-#endif
-#ifndef RTG_NODE_SPLIT
-#define RTG_NODE_SPLIT 1
-#endif
-RTG_HD int push_sorted(BvhStack& st, int c0, float f0, int c1, float f1, int c2, float f2,
-                       int c3, float f3) {
-  auto bits = [](float f) {
-    unsigned u;
-    memcpy(&u, &f, 4);
-    return u;
-  };
-  unsigned k0 = bits(f0), k1 = bits(f1), k2 = bits(f2), k3 = bits(f3);
-  auto cx = [](int& ca, unsigned& ka, int& cb, unsigned& kb) {
-    if (kb > ka) {
-      const int ct = ca; ca = cb; cb = ct;
-      const unsigned kt = ka; ka = kb; kb = kt;
-    }
-  };
-  if (RTG_BVH_SORT == 0) {  // full sort: the others pushed farthest first
-    cx(c0, k0, c1, k1);
-    cx(c2, k2, c3, k3);
-    cx(c0, k0, c2, k2);
-    cx(c1, k1, c3, k3);
-    cx(c1, k1, c2, k2);
-  } else {  // the nearest to c3 (an invalid child has child 0 and the largest key)
-    cx(c0, k0, c1, k1);
-    cx(c1, k1, c2, k2);
-    cx(c2, k2, c3, k3);
-  }
-  int nxt = 0;
-  auto put = [&](int c) {
-    if (c > 0) {
-      if (nxt > 0) st.push(nxt);
-      nxt = c;
-    }
-  };
-  put(c0);
-  put(c1);
-  put(c2);
-  put(c3);
-  return nxt;
-}
-
-// One node of a ray query: box tests of its child slots (reach `reachT` in
-// ray parameter units) and distance pruning + pass-1 screens of its sphere
-// slots (reach `reachD` in distance units); child nodes some active lane
-// still needs are ordered front to back (the nearest returned, the others
-// pushed), sphere slots are handed to `leaf(i, c, r2)` for lanes that pass.
-// `active`: the lane still queries.  Returns the next node (> 0) or 0.
+// costs 2.4 times an extra vector one), so:
+//  * the sphere slots run in one unrolled pass and the box slots in a
+//    second, each slot behind one wave-uniform test of its child word (an
+//    empty / box / sphere if-else costs the structurizer's flow instructions
+//    per slot: C5 -3.1 %, item 48);
+//  * the sphere slots take the reach and activity the node's earlier sphere
+//    slots left (`liveReach` = the closest query's minT, in ray units times
+//    `liveDn`; `liveBlk` = the shadow query's blocked lanes), and the box
+//    slots those the sphere slots left: still conservative (later visits use
+//    them anyway), and a leaf hit in the node can cull its siblings (items
+//    51-52).
 template <class Scene, class Leaf>
 RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned nd, bool active,
                         float reachT, float reachD, BvhStack& st, Leaf&& leaf,
@@ -1567,47 +1364,17 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
                         float liveDn = 0.f) {
   BvhRec r;
   sc.bvh_rec(nd * kBvhCopies + oct, r);
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_SALU)  // issue-cost probes (A/B builds)
-  {
-    unsigned pad;
-#pragma unroll
-    for (int k = 0; k < RTG_PAD_BVH_SALU; ++k) asm volatile("s_mov_b32 %0, 7" : "=s"(pad));  // no SCC write
-  }
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_NOP)
-  {
-#pragma unroll
-    for (int k = 0; k < RTG_PAD_BVH_NOP; ++k) asm volatile("s_nop 0");
-  }
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTG_PAD_BVH_VALU)
-  {
-    float pad;
-#pragma unroll
-    for (int k = 0; k < RTG_PAD_BVH_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, 2.0" : "=v"(pad));
-  }
-#endif
   int pc[4];
-  float pk[4];
-  float keyMax;  // bit pattern 0xFFFFFFFF: an invalid child sorts last (push_sorted)
-  {
-    const unsigned u = 0xFFFFFFFFu;
-    memcpy(&keyMax, &u, 4);
-  }
   auto box_slot = [&](int k, int x) {
     const float* g = &r.s[6 * k];
     sc.count(kUBvhSlot, 1);
     sc.count(shadowQ ? kCntBvhShadowNodeTests : kCntBvhNodeTests, 1);
     float tn;
-    // RTG_REACH_LIVE: the reach and activity after this node's sphere slots
-    const float rT = (RTG_REACH_LIVE && liveReach) ? *liveReach : reachT;
-    const bool act = (RTG_REACH_LIVE && liveBlk) ? (active && !*liveBlk) : active;
+    const float rT = liveReach ? *liveReach : reachT;
+    const bool act = liveBlk ? (active && !*liveBlk) : active;
     const bool pass = act && slab_pass(b, v3(g[0], g[1], g[2]), v3(g[3], g[4], g[5]), rT, tn);
     if (pass) sc.count(kUBvhPass, 1);
-    if (sc.any(pass)) {
-      pc[k] = x;
-      if (!RTG_BVH_OCT) pk[k] = sc.first_lane(tn);
-    }
+    if (sc.any(pass)) pc[k] = x;
   };
   auto sphere_slot = [&](int k, int x) {
     const float* g = &r.s[6 * k];
@@ -1619,51 +1386,33 @@ RTG_HD int bvh_ray_node(const Scene& sc, const RayQ& q, const BoxQ& b, unsigned 
     const float p2 = fmaf(p.x, p.x, fmaf(p.y, p.y, p.z * p.z));
     const float cs = p2 - g[3];
     const float v = fmaf(xd, xd, fmaf(-q.ap, cs, 0x1p-100f));  // pass1_rad
-    // RTG_LEAF_LIVE: the reach and activity the node's earlier sphere slots left
-    const float rD = (RTG_LEAF_LIVE && liveReach) ? *liveReach * liveDn : reachD;
-    const bool act = (RTG_LEAF_LIVE && liveBlk) ? (active && !*liveBlk) : active;
+    const float rD = liveReach ? *liveReach * liveDn : reachD;
+    const bool act = liveBlk ? (active && !*liveBlk) : active;
     if (act && !beyond(p2, g[5], rD) && !(v < 0.f) && !behind(0.5f * q.den, xd, cs, g[3]))
       leaf((unsigned)~x, c, g[4]);
   };
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    pc[k] = 0;
-    pk[k] = keyMax;
-  }
-  if (RTG_NODE_SPLIT) {  // sphere slots, then box slots: one test per slot and pass
+  for (int k = 0; k < 4; ++k) pc[k] = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r.ch[k] < 0) sphere_slot(k, r.ch[k]);  // wave-uniform
+  for (int k = 0; k < 4; ++k)
+    if (r.ch[k] < 0) sphere_slot(k, r.ch[k]);  // wave-uniform
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r.ch[k] > 0) box_slot(k, r.ch[k]);
-  } else {
+  for (int k = 0; k < 4; ++k)
+    if (r.ch[k] > 0) box_slot(k, r.ch[k]);
+  int nxt = 0;  // slots already front to back: the nearest next, the others pushed far first
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int x = r.ch[k];
-      if (x == 0) continue;  // wave-uniform
-      if (x > 0) box_slot(k, x);
-      else sphere_slot(k, x);
+  for (int k = 3; k >= 0; --k) {
+    if (pc[k] > 0) {
+      if (nxt > 0) st.push(nxt);
+      nxt = pc[k];
     }
   }
-  if (RTG_BVH_OCT) {  // slots already front to back: the nearest next, the others pushed far first
-    int nxt = 0;
-#pragma unroll
-    for (int k = 3; k >= 0; --k) {
-      if (pc[k] > 0) {
-        if (nxt > 0) st.push(nxt);
-        nxt = pc[k];
-      }
-    }
-    return nxt;
-  }
-  return push_sorted(st, pc[0], pk[0], pc[1], pk[1], pc[2], pk[2], pc[3], pk[3]);
+  return nxt;
 }
 
-// The direction octant of the wave's first lane (RTG_BVH_OCT's node copy).
+// The direction octant of the wave's first lane (the node copy it reads).
 template <class Scene>
 RTG_HD unsigned query_octant(const Scene& sc, const RayQ& q) {
-  if (!RTG_BVH_OCT) return 0u;
   const V3 d = sc.first_lane(q.d);
   return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
 }
@@ -1671,52 +1420,26 @@ RTG_HD unsigned query_octant(const Scene& sc, const RayQ& q) {
 // Closest-hit and shadow updates for an accepted root (BVH and list loops),
 // as selects: the exact (t, index) order and the reference's |t D|^2 < gap
 // test with no exec-mask branch, whose save/branch/restore costs scalar issue
-// (RTG_SEL_UPD=0: branches; with RTG_QUOT2, C5 -3.2 %).
-#ifndef RTG_SEL_UPD
-#define RTG_SEL_UPD 1
-#endif
-// The updates ignore `res` (RTG_RES_FREE=0: they test it): ray_sphere returns
-// exactly 10000 when it accepts no root, and minT <= 1000 and the shadow reach
-// 1000 are below that, so t < minT, t == minT and t < 1000 already imply res,
-// and the root test's flag is dead code (C5 -0.5 %).
-#ifndef RTG_RES_FREE
-#define RTG_RES_FREE 1
-#endif
-RTG_HD void take_closer(bool res, float t, int i, float& minT, int& best) {
-  if (RTG_RES_FREE) res = true;
-#if RTG_SEL_UPD
-  const bool b = res & ((t < minT) | ((t == minT) & (i < best)));
+// (C5 -3.2 %).  They need no root flag: ray_sphere
+// returns exactly 10000 when it accepts no root, and minT <= 1000 and the
+// shadow reach 1000 are below that, so t < minT, t == minT and t < 1000
+// already imply an accepted root (C5 -0.5 %, item 50).
+RTG_HD void take_closer(float t, int i, float& minT, int& best) {
+  const bool b = (t < minT) | ((t == minT) & (i < best));
   minT = b ? t : minT;
   best = b ? i : best;
-#else
-  if (res && (t < minT || (t == minT && i < best))) {
-    minT = t;
-    best = i;
-  }
-#endif
 }
-RTG_HD void take_blocker(bool res, float t, V3 d, float gap, bool& blk) {
-  if (RTG_RES_FREE) res = true;
-#if RTG_SEL_UPD
+RTG_HD void take_blocker(float t, V3 d, float gap, bool& blk) {
   const V3 dist = vsmul(t, d);
-  blk = blk | (res & (t < 1000.f) & (vdot(dist, dist) < gap));
-#else
-  if (res && t < 1000.f) {
-    const V3 dist = vsmul(t, d);
-    if (vdot(dist, dist) < gap) blk = true;
-  }
-#endif
+  blk = blk | ((t < 1000.f) & (vdot(dist, dist) < gap));
 }
 
-// (minT0, best0): a candidate already known (an accepted root of sphere
-// best0, or 1000 / -1): the answer is the lexicographic minimum of (t, i)
-// over every accepted root below 1000, so starting from any real candidate
-// gives the same answer with a shorter reach (closest_seeded).
+// Closest hit: the lexicographic minimum of (t, i) over every accepted root
+// below 1000 (minT from 1000, as calcIntersection).
 template <class Scene>
-RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 = 1000.f,
-                       int best0 = -1, bool active = true) {
-  float minT = minT0;
-  int best = best0;
+RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut) {
+  float minT = 1000.f;
+  int best = -1;
   const float dn = norm_up(q.den * 0.5f);
   const BoxQ b = make_boxq(q);
   BvhStack st(sc.bvh_stack());
@@ -1724,13 +1447,13 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut, float minT0 
   unsigned nd = 0;  // the root
   for (;;) {        // wave-uniform
     sc.count(kUBvhNode, 1);
-    const int nx = bvh_ray_node(sc, q, b, nd, active, minT, minT * dn, st,
+    const int nx = bvh_ray_node(sc, q, b, nd, true, minT, minT * dn, st,
                                 [&](unsigned i, V3 ce, float r2) {
       sc.count(kCntFullCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
-      take_closer(res, t, (int)i, minT, best);
+      const float t = ray_sphere_leaf(q, ce, r2, res);
+      take_closer(t, (int)i, minT, best);
     }, false, oct, &minT, nullptr, dn);
     if (nx > 0) {
       nd = (unsigned)nx;
@@ -1764,8 +1487,8 @@ RTG_HD bool blocked_bvh(const Scene& sc, const RayQ& q, float gap) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUBvhExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, ce, r2, res);
-      take_blocker(res, t, q.d, gap, blk);
+      const float t = ray_sphere_leaf(q, ce, r2, res);
+      take_blocker(t, q.d, gap, blk);
     }, true, oct, nullptr, &blk);
     if (sc.all(blk)) break;
     if (nx > 0) {
@@ -1846,23 +1569,19 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
     if (!blk && screen_ahead(q, r.c, r.rs)) {
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere_leaf<(RTG_NOROOT >= 2)>(q, r.c, r.r2, res);
-      take_blocker(res, t, q.d, gap, blk);
+      const float t = ray_sphere_leaf(q, r.c, r.r2, res);
+      take_blocker(t, q.d, gap, blk);
     }
   };
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
     ListRec r0, r1;
     sc.cap_rec2(k, r0, r1);
+    // the pair's second record past the list's end is the next list's (or
+    // the table's padding record): a real sphere can only block if it
+    // blocks, so testing it keeps the answer; one exit test per pair
+    // 
     step(r0);
-    if (RTG_LIST_PAIR) {
-      // the pair's second record past the list's end is the next list's (or
-      // the table's padding record): a real sphere can only block if it
-      // blocks, so testing it keeps the answer; one exit test per pair
-      step(r1);
-    } else {
-      if (sc.all(blk) || k + 1 >= k1) break;
-      step(r1);
-    }
+    step(r1);
     if (sc.all(blk)) break;
   }
   return blk;
@@ -1897,7 +1616,7 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
       sc.count(kUEnterExact, 1);
       bool rj;
       const float t = ray_sphere_leaf(q, r.c, r.r2, rj);
-      take_closer(rj, t, j, minT, best);
+      take_closer(t, j, minT, best);
     }
   };
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
@@ -1907,91 +1626,10 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
     // past the list's end: the next list's sphere (or the padding record);
     // the answer is the lexicographic minimum over every sphere, so a real
     // extra sphere keeps it
-    if (RTG_LIST_PAIR || k + 1 < k1) step(r1);
+    step(r1);
   }
   tOut = minT;
   return best;
-}
-
-// Closest hit of rays that start in sphere h's origin ball B''_h (every
-// active lane: a refraction child leaving h from its hit point P, P in h's
-// guard ball; or a reflection child from P + 0.01 rd), over h's neighbour
-// list (neighbour_lists, rtg_scene_pack.h): its records come in increasing
-// order of a certified lower bound delta on any accepted root's hit distance
-// t |d| from B''_h, so once a lane's best root has minT |d| < delta of the
-// next record (|d| rounded up, the product's rounding covered by the host's
-// delta (1 - 2^-20), rounded down), no later sphere can reach minT and the
-// lane's lexicographic minimum of (t, index) is the answer.  The list ends
-// with a terminator whose delta bounds every sphere left out (+inf when none
-// is); lanes it does not certify take the BVH from their best (closest_bvh,
-// certified lanes inactive).
-template <class Scene>
-RTG_HD int closest_near(const Scene& sc, const RayQ& q, int h, float& tOut) {
-  float minT = 1000.f;
-  int best = -1;
-  const float dn = norm_up(q.den * 0.5f);
-  unsigned k0, k1;
-  sc.nbr_range((unsigned)h, k0, k1);
-  bool cert = false;
-  auto step = [&](const ListRec& r) {
-    if (cert) return;
-    if (minT * dn < r.cr) {  // r.cr: the record's delta (1 - 2^-20), rounded down
-      cert = true;
-      return;
-    }
-    sc.count(kUNbrIter, 1);
-    if (screen_ahead(q, r.c, r.rs)) {
-      sc.count(kUBvhExact, 1);
-      bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj);
-      const int j = r.idx;
-      take_closer(rj, t, j, minT, best);
-    }
-  };
-  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
-    ListRec r0, r1;
-    sc.nbr_rec2(k, r0, r1);
-    step(r0);
-    if (sc.all(cert) || k + 1 >= k1) break;
-    step(r1);
-    if (sc.all(cert)) break;
-  }
-  tOut = minT;
-  if (sc.all(cert)) return best;
-  sc.count(kCntFullQ, 1);
-  return closest_bvh(sc, q, tOut, minT, best, !cert);
-}
-
-// Closest hit of rays that leave sphere h (every active lane: its hit point
-// P on h is the origin; refraction children that exit h, and (RTG_SEED_EXIT
-// >= 2) reflection children): the spheres that overlap h (h's overlap list)
-// are the likeliest first hits (P usually lies inside some of them in a dense
-// cluster), so their lexicographic minimum of (t, index) seeds the BVH query,
-// whose reach then starts at that t.  Any seed gives the same answer
-// (closest_bvh), so the list needs no geometric condition.
-template <class Scene>
-RTG_HD int closest_seeded(const Scene& sc, const RayQ& q, int h, float& tOut) {
-  float minT = 1000.f;
-  int best = -1;
-  unsigned k0, k1;
-  sc.ov_range((unsigned)h, k0, k1);
-  auto step = [&](const ListRec& r) {
-    sc.count(kUOvIter, 1);
-    if (screen_ahead(q, r.c, r.rs)) {
-      sc.count(kUBvhExact, 1);
-      bool rj;
-      const float t = ray_sphere(q, r.c, r.r2, rj);
-      const int j = r.idx;
-      take_closer(rj, t, j, minT, best);
-    }
-  };
-  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
-    ListRec r0, r1;
-    sc.ov_rec2(k, r0, r1);
-    step(r0);
-    if (k + 1 < k1) step(r1);
-  }
-  return closest_bvh(sc, q, tOut, minT, best);
 }
 
 // primary_container (raytracer.h:245-270) for refraction test points of hits
@@ -2016,14 +1654,9 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
     ListRec r0, r1;
     sc.ov_rec2(k, r0, r1);
     step(r0);
-    if (RTG_LIST_PAIR) {
-      // a sphere past the list's end (the next list's) cannot contain the
-      // point (primary_container_sel's argument: every container is listed)
-      step(r1);
-    } else {
-      if (sc.all(found >= 0) || k + 1 >= k1) break;
-      step(r1);
-    }
+    // a sphere past the list's end (the next list's) cannot contain the
+    // point (primary_container_sel's argument: every container is listed)
+    step(r1);
     if (sc.all(found >= 0)) break;
   }
   return found;
@@ -2131,7 +1764,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
       sc.count(kCntShadowCand, 1);
       sc.count(kUShdExact, 1);
       bool res;
-      const float t = ray_sphere_k<kFast, (RTG_NOROOT >= 1)>(q, c, r2, res);
+      const float t = ray_sphere_k<kFast, true>(q, c, r2, res);
       if (res && t < 1000.f) {
         const V3 dist = vsmul(t, q.d);
         if (vdot(dist, dist) < gap) blk = true;

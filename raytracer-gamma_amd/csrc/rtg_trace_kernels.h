@@ -23,9 +23,6 @@ namespace rtg {
 
 constexpr int kBlock = 256;
 
-#ifndef RTG_BVH_LOAD2  // A/B builds: DevScene::bvh_rec's paired node loads
-#define RTG_BVH_LOAD2 0
-#endif
 // Materials staged in LDS when the table fits (n+1 records of 32 B).
 constexpr unsigned kLdsMatMax = 1024 + 1;  // => <= 48 KiB of LDS per workgroup
 
@@ -190,8 +187,6 @@ struct DevScene {
   int* bvhStk;        // this wave's 64-entry LDS traversal stack (BVH scenes)
   cfloat_p capRec, ovRec;  // sphere lists of BVH scenes (sphere_lists) or null
   cuint_p capOff, ovOff;
-  cfloat_p nbrRec;  // neighbour lists of BVH scenes (neighbour_lists) or null
-  cuint_p nbrOff;
   unsigned n, m;
   unsigned n4;  // geometry records incl. NaN padding to a multiple of 4
 
@@ -295,20 +290,6 @@ struct DevScene {
   __device__ __forceinline__ void ov_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
   }
-  // Neighbour lists (neighbour_lists, rtg_scene_pack.h): h's records are
-  // nbrOff[h] .. nbrOff[h + 1] (the last one h's terminator).
-  __device__ __forceinline__ bool has_nbr() const {
-    if constexpr (kBvh) return nbrOff != nullptr;
-    else return false;
-  }
-  __device__ __forceinline__ void nbr_range(unsigned h, unsigned& k0, unsigned& k1) const {
-    const cuint_p o = uidx(nbrOff, h);
-    k0 = o[0];
-    k1 = o[1];
-  }
-  __device__ __forceinline__ void nbr_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
-    list_rec2(nbrRec, k, r0, r1);
-  }
   __device__ __forceinline__ V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
                                         float& rf) const {
     return list_rec(capRec, k, rs, r2, cr, idx, rf);
@@ -317,24 +298,13 @@ struct DevScene {
                                        float& rf) const {
     return list_rec(ovRec, k, rs, r2, cr, idx, rf);
   }
-  // Node nd's record (BvhRec, rtg_trace.h): two 64-byte scalar loads.
-  // RTG_BVH_LOAD2 (A/B builds): both issued back to back in one asm block
-  // with one wait, into disjoint registers (the compiler's own schedule waits
-  // for the first before issuing the second: two round trips per node).
+  // Node copy nd's record (BvhRec, rtg_trace.h): two 64-byte scalar loads
+  // (issuing both from one asm block with one wait measured slower, DESIGN.md
+  // §4 item 44).
   __device__ __forceinline__ void bvh_rec(unsigned nd, BvhRec& r) const {
     typedef float f16 __attribute__((ext_vector_type(16)));
-#if RTG_BVH_LOAD2
-    f16 a, b;
-    asm volatile(
-        "s_load_dwordx16 %0, %2, %3\n\t"
-        "s_load_dwordx16 %1, %2, %3 offset:0x40\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&s"(a), "=&s"(b)
-        : "s"(bvhNodes), "s"(nd * (unsigned)(kBvhWords * 4)));
-#else
     const RTG_CONST f16* p = (const RTG_CONST f16*)fidx(bvhNodes, kBvhWords * nd);
     const f16 a = p[0], b = p[1];
-#endif
 #pragma unroll
     for (int k = 0; k < 16; ++k) r.s[k] = a[k];
 #pragma unroll
@@ -530,8 +500,6 @@ struct KernelArgs {
   const unsigned* capOff;
   const float* ovRec;
   const unsigned* ovOff;
-  const float* nbrRec;    // neighbour lists (PackedScene::nbr*) or null
-  const unsigned* nbrOff;
   unsigned n, m, n4;
   Camera cam;
   unsigned W, rowsLocal, rowBlock, shard, nShards;
@@ -664,8 +632,6 @@ __device__ __forceinline__ void stage_scene(const KernelArgs& a, Sc& sc) {
   sc.capOff = (cuint_p)a.capOff;
   sc.ovRec = (cfloat_p)a.ovRec;
   sc.ovOff = (cuint_p)a.ovOff;
-  sc.nbrRec = (cfloat_p)a.nbrRec;
-  sc.nbrOff = (cuint_p)a.nbrOff;
   // BVH scenes: 64 stack entries per wave after the frames and scene tables
   // (the launcher adds them to the LDS size).
   sc.bvhStk = reinterpret_cast<int*>(sceneLds + (kLds ? (a.n + 1) * 2 + a.n4 : 0)) +

@@ -55,6 +55,7 @@ EXPORTED = [
     "rtg_render", "rtg_context_create", "rtg_context_destroy", "rtg_context_set_scene",
     "rtg_shard_rows", "rtg_shard_global_row", "rtg_render_device", "rtg_render_rows_device",
     "rtg_render_rows", "rtg_set_launch_opts", "rtg_diag_read", "rtg_diag_timeline", "rtg_diag_counts",
+    "rtg_diag_group_list",
     "rtg_context_scene_stats",
     "rtg_max_colour", "rtg_max_colour_device", "rtg_ppm_bytes", "rtg_ppm_bytes_device",
     "rtg_save_ppm", "rtg_make_material", "rtg_scene_generate", "rtg_assemble_shards_device",
@@ -77,7 +78,7 @@ UNIT_NAMES = [
     "U.maskIter", "U.node", "U.shade", "U.light", "U.shadow", "U.lit", "U.refr", "U.refrLeaf",
     "U.push", "U.descend", "U.unwind", "U.sample", "U.bvhPass",
     "U.capIter", "U.ovIter", "D.shdSame", "D.enterAll", "D.enterSame", "D.contSame",
-    "U.lightDir", "U.nbrIter", "D.insig", "D.insigAll",
+    "U.lightDir", "D.insig", "D.insigAll",
 ]
 
 
@@ -114,6 +115,8 @@ def lib() -> ctypes.CDLL:
         L.rtg_context_set_semantics.argtypes = [vp, i]
         L.rtg_diag_read.argtypes = [vp, vp, i]
         L.rtg_diag_timeline.argtypes = [vp, vp, sz, vp]
+        if hasattr(L, "rtg_diag_group_list"):  # (A/B libraries of older revisions lack it)
+            L.rtg_diag_group_list.argtypes = [vp, vp, vp, vp, vp, sz, vp]
         # round-3 entry points; an RTG_LIB build from before them (same-box A/B
         # of older kernels, tools/ab_bench.sh) loads without them
         for name, at in (("rtg_diag_counts", [vp, vp, i, i]),
@@ -420,6 +423,24 @@ class Context:
         _check(lib().rtg_diag_timeline(self._h, ctypes.c_void_p(out.ctypes.data), cap,
                                        ctypes.byref(cnt)), "rtg_diag_timeline")
         return out[:min(cap, cnt.value)]
+
+    def diag_group_list(self, cap: int = 1 << 26):
+        """The last compacted launch: {cost[groups], list[2 groups], sel[2 groups],
+        runs[4]} (rtg_diag_group_list; costs in 100 MHz ticks)."""
+        n = ctypes.c_size_t(0)
+        _check(lib().rtg_diag_group_list(self._h, None, None, None, None, 0, ctypes.byref(n)),
+               "rtg_diag_group_list")
+        g = min(cap, n.value)
+        cost = np.zeros(g, np.uint32)
+        lst = np.zeros(2 * g, np.uint32)
+        sel = np.zeros(2 * g, np.uint64)
+        runs = np.zeros(4, np.uint32)
+        _check(lib().rtg_diag_group_list(self._h, ctypes.c_void_p(cost.ctypes.data),
+                                         ctypes.c_void_p(lst.ctypes.data),
+                                         ctypes.c_void_p(sel.ctypes.data),
+                                         ctypes.c_void_p(runs.ctypes.data), g, ctypes.byref(n)),
+               "rtg_diag_group_list")
+        return {"cost": cost, "list": lst, "sel": sel, "runs": runs}
 
     def render_device(self, width, height, dst_ptr: int, zoom=-4.0, alias_factor=3.0,
                       stack_size=6, row_block=16, shard=0, n_shards=1, stream: int = 0):

@@ -96,9 +96,6 @@ UNIT_COST = {
     # container_list): one record's pass-1 screen (+ not-blocked) or containment test
     "U.capIter": 13,
     "U.ovIter": 13,
-    # closest_near: one neighbour-list record's certificate (minT |d| < delta,
-    # 2) and pass-1 screen (12)
-    "U.nbrIter": 15,
     # lane -> pixel / sample (6), sample_dir + vnorm (38), scaled sum, ordered
     # pixel sums (3 + 27), NaN canonicalisation and row bookkeeping (6)
     "U.sample": 80,

@@ -64,16 +64,6 @@ struct HostScene {
   void ov_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
   }
-  const float* nbrRec = nullptr;
-  const unsigned* nbrOff = nullptr;
-  bool has_nbr() const { return nbrOff != nullptr; }
-  void nbr_range(unsigned h, unsigned& k0, unsigned& k1) const {
-    k0 = nbrOff[h];
-    k1 = nbrOff[h + 1];
-  }
-  void nbr_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
-    list_rec2(nbrRec, k, r0, r1);
-  }
   rtg::V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
     return list_rec(capRec, k, rs, r2, cr, idx, rf);
   }
@@ -182,7 +172,6 @@ struct HostScene {
 int g_variant = 0;
 bool g_useBvh = true;
 bool g_useLists = true;  // the sphere lists of BVH scenes (coherent-wave queries)
-bool g_useNbr = true;    // the neighbour lists of BVH scenes (closest_near)
 double g_boundM = 0.0;          // hostsim_bvh_bound_check: box margin probe (0: 2^-8)
 
 template <int S>
@@ -260,7 +249,6 @@ void run(const HostScene& sc, const rtg::Camera& cam, unsigned W, unsigned y, fl
 extern "C" void hostsim_set_variant(int v) { g_variant = v; }
 extern "C" void hostsim_use_bvh(int on) { g_useBvh = on != 0; }
 extern "C" void hostsim_use_lists(int on) { g_useLists = on != 0; }
-extern "C" void hostsim_use_nbr(int on) { g_useNbr = on != 0; }
 extern "C" void hostsim_capsule_back_slack(double s) { rtg::g_capsuleBackSlack = s; }
 extern "C" void hostsim_bound_margin(double m) { g_boundM = m; }
 // Operation counters of the kernel traversal (rtg_trace.h kCnt*), summed over
@@ -296,10 +284,6 @@ extern "C" int hostsim_render_rows(const rtg_sphere* spheres, unsigned n,
       sc.capOff = ps.capOff.data();
       sc.ovRec = ps.ovRec.data();
       sc.ovOff = ps.ovOff.data();
-      if (!ps.nbrOff.empty() && g_useNbr) {
-        sc.nbrRec = ps.nbrRec.data();
-        sc.nbrOff = ps.nbrOff.data();
-      }
     }
   }
   for (unsigned k = 0; k < nrows; ++k) {

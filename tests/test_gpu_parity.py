@@ -353,6 +353,41 @@ def test_launch_order_feedback_keeps_frames(R, golden, torch_cuda):
     ctx.close()
 
 
+def test_failed_launch_leaves_slots_consistent(R, golden, torch_cuda):
+    """A render that fails after the launch scratch is chosen (the counting
+    build has no kernel for a maskless compacted scene: an empty scene) leaves
+    the slot ring and the cost entries as the last good launch left them, so
+    more good renders than the ring holds (rtg_context::kSlots = 4) still give
+    the golden frame (the counter set a slot's next cull pass adds
+    to must have been zeroed by a trace kernel)."""
+    torch = torch_cuda
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    W, H, S = c["W"], c["H"], c["stack_size"]
+    ctx = R.Context(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+
+    def good(k):
+        for _ in range(k):
+            out.fill_(5.0)
+            ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=stream)
+            torch.cuda.synchronize()
+            assert canon_md5(out.cpu().numpy()) == c["fb_md5"]
+
+    ctx.set_scene(sph, lg)
+    good(2)
+    ctx.set_scene(sph[:0], lg)  # no spheres: compacted, no masks
+    ctx.set_variant(120)
+    for _ in range(3):
+        with pytest.raises(R.RtgError):
+            ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=stream)
+    ctx.set_variant(0)
+    ctx.set_scene(sph, lg)
+    good(9)
+    ctx.close()
+
+
 @pytest.mark.parametrize("variant", [0, 9])
 def test_variant_full_frames(R, golden, torch_cuda, variant):
     """Kernel mappings over whole frames, sharded frames, row lists and
@@ -730,6 +765,51 @@ def test_opencl_semantics_vs_oracle(R, oracle, torch_cuda):
     with pytest.raises(R.RtgError):
         ctx.set_semantics(7)
     ctx.close()
+
+
+def test_opencl_reference_kernel_pins_oracle(R, oracle, torch_cuda):
+    """The reference's OWN OpenCL kernel (raytrace_kernel.cl:870-973, compiled
+    for gfx950 in place from /root/reference by oracle/build_ref_cl.sh with
+    correctly rounded division/sqrt and no contraction, launched as a HIP
+    module: tests/clref.py) against the OpenCL-semantics oracle
+    (oracle_render_rows_cl) and the kernel's kCL mode (variant 50 and its
+    nAA > 8 fallback 59), bit for bit: the main.cpp scene and seeded random
+    scenes of up to 20 spheres, several sizes, aliasFactors and zooms."""
+    import clref
+    torch = torch_cuda
+    if not os.path.exists(clref.HSACO):
+        pytest.skip("oracle/_ref/rtg_ref_cl.hsaco not built (needs /root/reference at build)")
+    ref = clref.RefCL()
+    ctx = R.Context(0)
+    ctx.set_semantics(ctx.SEMANTICS_OPENCL)
+    rng = np.random.default_rng(5150)
+    cases = [(3.0, -4.0, None, 160, 120)] + [None] * 15
+    try:
+        for trial, case in enumerate(cases):
+            if case is None:
+                aa = float(rng.choice([1.0, 2.0, 3.0, 9.0]))
+                zoom = float(rng.choice([-4.0, 3.0]))
+                n, m = int(rng.integers(0, 21)), int(rng.integers(0, 5))
+                sph, lg = random_scene(rng, n, m)
+                if zoom > 0:
+                    sph["pos"][:, 2] *= -1.0
+                W, H = int(rng.integers(1, 64)), int(rng.integers(1, 40))
+            else:
+                aa, zoom, _, W, H = case
+                sph, lg = R.reference_scene()
+            want = ref.render(torch, sph, lg, W, H, zoom=zoom, aa=aa)
+            orc = oracle.render_cl(sph, lg, W, H, 5, aa=aa, zoom=zoom)
+            assert bits_equal(orc, want), (trial, W, H, aa, first_mismatch(orc, want))
+            ctx.set_scene(sph, lg)
+            out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+            ctx.render_device(W, H, out.data_ptr(), zoom=zoom, alias_factor=aa, stack_size=5,
+                              stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            assert bits_equal(got, want), (trial, W, H, aa, first_mismatch(got, want))
+    finally:
+        ctx.close()
+        ref.close()
 
 
 def test_host_driver_opencl_semantics_ppm(R, oracle, tmp_path):

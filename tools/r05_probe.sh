@@ -28,6 +28,12 @@ for k in ("U.node", "U.bvhNode", "U.bvhSlot", "U.bvhExact", "U.capIter", "U.ovIt
 print("ms", d["ms_per_step"], "first", d.get("first_launch_ms"), "frac", r.get("frac"))
 PY
 done
+if [ -n "$COST_DUMP" ]; then
+  for c in $COST_DUMP; do
+    echo "== cost dump $c" &&
+    timeout -k 10 300 python tools/cost_study.py --dump --config $c --out $OUT/cost_$c.npz > $OUT/cost_$c.txt 2>&1; rc=$?; tail -2 $OUT/cost_$c.txt; [ $rc -eq 0 ] || exit $rc
+  done
+fi
 if [ -n "$MEM_PMC" ]; then
   echo "== memory PMC c3" &&
   TAG=${TAG}_mem CFG=c3 PMC_GROUPS="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum|TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum|FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA" bash tools/gpu_pmc.sh > $OUT/pmc_mem.log 2>&1; rc=$?; tail -30 $OUT/pmc_mem.log; [ $rc -eq 0 ] || exit $rc
