@@ -450,6 +450,27 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     mpx = W * H / (elapsed / args.steps) / 1e6
 
+    # The first launches of a fresh frame geometry on a WARM GPU (after the
+    # timed region; set_scene starts a new scene generation, so the launch-
+    # order feedback starts empty).  first_launch_ms above is the same launch
+    # at process start, where the GPU is still ramping its clocks: the cold
+    # probe (tools/cold_probe.py, profiles/r05/cold_probe_c3.txt) puts the
+    # feedback-ordered steady launch at process start ~20 % above the warm one,
+    # so the two figures separate the launch path's own cold cost from the
+    # GPU's power-state ramp.
+    fresh_ms = None
+    if world == 1:
+        fresh_ms = []
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ctx.set_scene(sph, lg)
+        for _ in range(3):
+            torch.cuda.synchronize()
+            e0.record(stream)
+            step()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            fresh_ms.append(round(e0.elapsed_time(e1), 4))
+
     diag = None
     if args.diag and world == 1:
         ctx.set_variant(args.diag)
@@ -664,10 +685,21 @@ def main():
                 if vi:
                     # the same roofline from the hardware's count of executed
                     # VALU wave instructions (x 64 lanes) per launch, over this
-                    # run's mean kernel time: the model-free form of `frac`
+                    # run's mean kernel time.  It is the headline `frac` when
+                    # present (instruction counts are the same on any box for
+                    # these sources and this frame); the counting model's
+                    # stays beside it (frac_model) with its per-unit split.
                     ach_pmc = vi * 64 / (kern_ms * 1e-3) / 1e12
                     roof["achieved_pmc"] = round(ach_pmc, 3)
                     roof["frac_pmc"] = round(ach_pmc / VALU_PEAK_TOPS, 4)
+                    if roof.get("frac") is not None:
+                        roof["achieved_model"] = roof["achieved"]
+                        roof["frac_model"] = roof["frac"]
+                    roof["achieved"] = roof["achieved_pmc"]
+                    roof["frac"] = roof["frac_pmc"]
+                    roof["frac_source"] = ("PMC SQ_INSTS_VALU x 64 per launch "
+                                           f"({os.path.relpath(pmc, ROOT)}) / mean kernel time "
+                                           f"{kern_ms:.4f} ms (HIP events)")
                 roof["traffic_note"] = ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch "
                                         f"({os.path.relpath(pmc, ROOT)})")
 
@@ -687,6 +719,8 @@ def main():
         "kernel_ms": round(kern_ms, 4), "kernel_ms_max_rank": round(kern_max_ms, 4),
         "first_launch_ms": round(first_ms, 4) if first_ms is not None else None,
         "first_launch_process_ms": round(first_proc_ms, 4) if first_proc_ms is not None else None,
+        "first_launch_warm_gpu_ms": fresh_ms[0] if fresh_ms else None,
+        "fresh_geometry_launches_warm_ms": fresh_ms,
         "timed_launches": {"first": 2 + args.warmup if world == 1 else None,
                            "count": args.steps,
                            "note": "trace-kernel dispatches [first, first + count) of this "

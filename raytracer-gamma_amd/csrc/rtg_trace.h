@@ -235,6 +235,7 @@ enum : int { kCntSamples = 0, kCntPrimQ, kCntPrimSel, kCntPrimCand, kCntEnterQ, 
              kULightDir,    // matte_light: a light no facing-away test excluded (direction)
              kUDiagInsig,     // (diagnostic) stage-0 query; lane value: intensity insignificant
              kUDiagInsigAll,  // (diagnostic) stage-0 query whose every active lane is insignificant
+             kUWave,        // one wave of the sample kernel: prologue, list walk, epilogue
              kCntSlots };
 enum : int { kProbeClosest = 0, kProbeShadow = 1, kProbeRefraction = 2, kProbeTotal = 3,
              kProbeMatte = 4, kProbePush = 5, kProbeUnwind = 6, kProbeShade = 7,

@@ -965,6 +965,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
            kCount>
       sc;
   sc.count_reset();
+  sc.count(kUWave, 1);  // every wave, those past the listed groups included
   const unsigned t0 = (unsigned)__builtin_amdgcn_s_memrealtime();
   stage_scene<S, kLds, kThreads>(a, sc);
   if constexpr (kVariant == 20) sc.cone = nullptr;  // A/B: no secondary-ray cone cull

@@ -78,7 +78,7 @@ UNIT_NAMES = [
     "U.maskIter", "U.node", "U.shade", "U.light", "U.shadow", "U.lit", "U.refr", "U.refrLeaf",
     "U.push", "U.descend", "U.unwind", "U.sample", "U.bvhPass",
     "U.capIter", "U.ovIter", "D.shdSame", "D.enterAll", "D.enterSame", "D.contSame",
-    "U.lightDir", "D.insig", "D.insigAll",
+    "U.lightDir", "D.insig", "D.insigAll", "U.wave",
 ]
 
 
