@@ -587,6 +587,10 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
 template <class Scene>
 RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
+RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h);
+template <class Scene>
+RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT);
+template <class Scene>
 RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok);
 
 // Does the scene type run the BVH kernels (DevScene::kIsBvh)?  Host scene
@@ -639,10 +643,11 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
           sc.count(kCntShadowQ, 1);
           sc.count(kCntShadowSel, __builtin_popcountll(su));
           blk = blocked_sel(sc, P, dir, gap, su);
-        } else if (sc.has_lists() && sc.all(guardOK) && sc.all(sc.first_lane_i(hit) == hit)) {
-          // BVH scene, coherent wave: sphere hit's capsule list for light l
-          sc.count(kUDiagShdSame, 1);
-          blk = blocked_cap(sc, P, dir, gap, l, sc.first_lane_i(hit));
+        } else if (sc.has_lists() && sc.all(guardOK)) {
+          // BVH scene: each lane's hit sphere's capsule list for light l, the
+          // wave's distinct hit spheres in turn (blocked_cap_lanes)
+          if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagShdSame, 1);
+          blk = blocked_cap_lanes(sc, P, dir, gap, l, hit);
         } else {
           blk = query_blocked<2>(sc, P, dir, gap);
         }
@@ -770,11 +775,11 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
     tgt = primary_container_sel(sc, testPt, cu, nTgt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
   } else if (hit >= 0 && sc.has_lists() &&
-             sc.all(guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax) &&
-             sc.all(sc.first_lane_i(hit) == hit)) {
-    // BVH scene, coherent wave: the first containing sphere of hit's overlap list
-    sc.count(kUDiagContSame, 1);
-    tgt = container_list(sc, testPt, sc.first_lane_i(hit), nTgt);
+             sc.all(guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax)) {
+    // BVH scene: the first containing sphere of each lane's hit sphere's
+    // overlap list, the wave's distinct hit spheres in turn (container_lanes)
+    if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagContSame, 1);
+    tgt = container_lanes(sc, testPt, hit, nTgt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
   } else {
     sc.count(kCntContainFull, 1);
@@ -1659,6 +1664,49 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
     // point (primary_container_sel's argument: every container is listed)
     step(r1);
     if (sc.all(found >= 0)) break;
+  }
+  return found;
+}
+
+// The list queries above for waves whose lanes hit different spheres (every
+// lane's point in its own sphere's guard ball): the wave takes its distinct
+// spheres in turn, each walked by the lanes on it (the others inactive), up
+// to kListWalks of them; lanes left after that take the BVH query.  The
+// answer is each lane's own list answer, so the frame is the same as with
+// the BVH (the lists' arguments hold per sphere).  A coherent wave is one
+// walk.
+constexpr int kListWalks = 4;
+template <class Scene>
+RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h) {
+  bool blk = false;
+  bool todo = true;
+  for (int k = 0; k < kListWalks; ++k) {  // wave-uniform
+    const int h0 = sc.lane_with(h, todo);
+    if (todo && h == h0) {
+      blk = blocked_cap(sc, o, d, gap, l, h0);
+      todo = false;
+    }
+    if (!sc.any(todo)) return blk;
+  }
+  if (todo) blk = query_blocked<2>(sc, o, d, gap);
+  return blk;
+}
+template <class Scene>
+RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT) {
+  int found = -1;
+  bool todo = true;
+  for (int k = 0; k < kListWalks; ++k) {  // wave-uniform
+    const int h0 = sc.lane_with(h, todo);
+    if (todo && h == h0) {
+      found = container_list(sc, pt, h0, nT);
+      todo = false;
+    }
+    if (!sc.any(todo)) return found;
+  }
+  if (todo) {
+    sc.count(kCntContainFull, 1);
+    found = primary_container(sc, pt);
+    nT = sc.refr(found < 0 ? (int)sc.n : found);
   }
   return found;
 }

@@ -319,6 +319,10 @@ struct DevScene {
   __device__ __forceinline__ float first_lane(float v) const {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
   }
+  // v of the first active lane with `pred` (some active lane has it).
+  __device__ __forceinline__ int lane_with(int v, bool pred) const {
+    return __builtin_amdgcn_readlane(v, (int)__builtin_ctzll(__ballot(pred)));
+  }
   __device__ __forceinline__ int first_lane_i(int v) const {
     return __builtin_amdgcn_readfirstlane(v);
   }
@@ -579,13 +583,17 @@ __device__ __forceinline__ float canon_nan(float v) {
 // VGPRs) where the LDS image of S-1 frame levels still admits 7 waves per
 // SIMD (S <= 6 with a small scene); measured +1-2 % over the unconstrained
 // 78-VGPR build at 6 waves/SIMD (C3, tile kernel).
-template <int S, int kVariant>
+// BVH kernels above S = 6 (C5: S = 8): 6 waves per SIMD, which their LDS
+// image (S - 2 frame levels + the traversal stack, 6.25 KB at S = 8) admits
+// (<= 80 VGPRs).
+template <int S, int kVariant, bool kBvh = false>
 #ifndef RTG_DEFAULT_MIN_WAVES  // compiler-setting A/B builds (tools/ab_build.sh) only
 #define RTG_DEFAULT_MIN_WAVES 7
 #endif
 struct MinWaves {
   static constexpr int value =
       (kVariant == 120) ? 1  // counting build: its counters take registers
+      : (kBvh && (kVariant == 0 || kVariant == 50) && S > 6) ? 6
       : (kVariant == 18 && S <= 6) ? 8
       : (kVariant == 0 && S <= 6) ? RTG_DEFAULT_MIN_WAVES
       : ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
@@ -1035,7 +1043,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
 
 template <int S, bool kLds, int kVariant, bool kBvh = false, bool kList = false,
           bool kMasks = false>
-__global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant>::value))
+__global__ __launch_bounds__(SampleThreads<kVariant>::value, (MinWaves<S, kVariant, kBvh>::value))
 void trace_samples_kernel(const KernelArgs a) {
   trace_samples_body<S, kLds, kVariant, kBvh, kList, kMasks>(a);
 }

@@ -89,6 +89,7 @@ struct HostScene {
   }
   float first_lane(float v) const { return v; }
   int first_lane_i(int v) const { return v; }
+  int lane_with(int v, bool) const { return v; }
   rtg::V3 sphere(unsigned i, float& r2) const {
     const float* g = geom + 4 * i;
     r2 = g[3];
