@@ -589,6 +589,11 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
 RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h);
 template <class Scene>
+RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut);
+// Most distinct spheres a wave walks the per-sphere lists of (blocked_cap_lanes
+// and friends) before its remaining lanes take the BVH.
+constexpr int kListWalks = 4;
+template <class Scene>
 RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
 RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok);
@@ -896,15 +901,33 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         sc.count(kCntFullQ, 1);
         hit = query_closest<2>(sc, o, d, t);
       }
-    } else if (Q == 4 && sc.has_lists() && sc.all(enterH >= 0) &&
-               sc.all(sc.first_lane_i(enterH) == enterH)) {
-      // BVH scene, coherent wave of rays that entered one sphere: it and its
-      // overlap list (closest_enter_list), else the BVH
-      sc.count(kUDiagEnterSame, 1);
-      bool ok;
+    } else if (Q == 4 && sc.has_lists() && sc.any(enterH >= 0)) {
+      // BVH scene, rays that entered a sphere: each lane's sphere and its
+      // overlap list (closest_enter_list), the wave's distinct spheres in
+      // turn; the other lanes, and the lanes a list does not settle, the BVH
+      if (sc.all(enterH >= 0) && sc.all(sc.first_lane_i(enterH) == enterH))
+        sc.count(kUDiagEnterSame, 1);
+      const RayQ q = make_query(o, d);
       sc.count(kUQuery, 1);
-      hit = closest_enter_list(sc, make_query(o, d), sc.first_lane_i(enterH), t, ok);
-      if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
+      bool todo = enterH >= 0, done = false;
+      hit = -1;
+      t = 1000.f;
+      for (int k = 0; k < kListWalks && sc.any(todo); ++k) {  // wave-uniform
+        const int h0 = sc.lane_with(enterH, todo);
+        if (todo && enterH == h0) {
+          bool ok;
+          const int hh = closest_enter_list(sc, q, h0, t, ok);
+          if (sc.all(ok)) {
+            hit = hh;
+            done = true;
+          }
+          todo = false;
+        }
+      }
+      if (!done) {
+        sc.count(kCntFullQ, 1);
+        hit = closest_bvh(sc, q, t);
+      }
     } else {
       if (sc.has_bvh() && sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
       sc.count(kCntFullQ, 1);
@@ -1675,7 +1698,6 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
 // answer is each lane's own list answer, so the frame is the same as with
 // the BVH (the lists' arguments hold per sphere).  A coherent wave is one
 // walk.
-constexpr int kListWalks = 4;
 template <class Scene>
 RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h) {
   bool blk = false;
