@@ -131,10 +131,15 @@ def hostsim():
         os.path.join(ROOT, "raytracer-gamma_amd", "csrc", f) for f in
         ("rtg_trace.h", "rtg_scene_pack.h", "rtg_internal.h")]
     if not os.path.exists(so) or any(os.path.getmtime(d) > os.path.getmtime(so) for d in deps):
+        # built under a private name and renamed into place: parallel test
+        # workers (pytest -n) may rebuild at once, and none may load a
+        # half-written library
+        tmp = "%s.%d.tmp" % (so, os.getpid())
         subprocess.run(["g++", "-O2", "-mfma", "-ffp-contract=off", "-fno-fast-math", "-std=c++17",
                         "-fPIC", "-shared", *defs, "-I" + os.path.join(ROOT, "include"),
-                        "-I" + os.path.join(ROOT, "raytracer-gamma_amd", "csrc"), src, "-o", so],
+                        "-I" + os.path.join(ROOT, "raytracer-gamma_amd", "csrc"), src, "-o", tmp],
                        check=True)
+        os.replace(tmp, so)
     return ctypes.CDLL(so)
 
 
