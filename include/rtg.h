@@ -233,10 +233,11 @@ int rtg_diag_timeline(rtg_context* ctx, unsigned* out4, size_t cap, size_t* coun
  * studies, tools/cost_study.py): *groups = its pixel groups; cost[g] (cap
  * entries at most) the trace time of group g in s_memrealtime ticks (100 MHz)
  * as its cost table holds it (0 when the launch had none; a group not listed
- * keeps a stale value), list / sel (2 x groups entries each) the listed group
- * indices and sphere masks by list position, runs[4] the four run lengths.
- * Any output pointer may be null.  RTG_ERR_INVALID when the context has made
- * no compacted launch. */
+ * keeps a stale value), list / sel (min(cap, groups) entries each) the listed
+ * group indices and sphere masks in the order the trace kernel's waves take
+ * them (runs[0] + ... + runs[3] entries), runs[4] the four run lengths summed
+ * over the list's partitions.  Any output pointer may be null.
+ * RTG_ERR_INVALID when the context has made no compacted launch. */
 int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
                         unsigned long long* sel, unsigned* runs, size_t cap, size_t* groups);
 

@@ -149,32 +149,44 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
 }
 
 // A block takes R x 256 consecutive groups (one per lane per round) and
-// appends its live ones with one atomic per run: the atomics on the counters
-// serialise in L2, so one per wave cost ~70 us on C3.  R (the launch picks
-// 1, 2 or 4) keeps at least ~4 blocks per CU: with R = 4 a C2 frame's pass
-// had 290 blocks (about one wave per SIMD) and took 24 us, latency-bound.
+// appends its live ones with one atomic per run, in one of kListParts list
+// partitions (block b: partition b % kListParts), each with its own run
+// counters and cost sum on a cache line of its own.  Device-scope atomics on
+// one address serialise (tools/cull_micro.hip, 1158 workgroups: one address
+// 15.1 us, 8 lines 4.5, 32 lines 3.7, no atomic 3.7): with the whole list on
+// one set of counters the C2 pass took 21 us, 11 of them queued atomics.
+// R (the launch picks 1, 2 or 4) keeps at least ~4 blocks per CU: with R = 4
+// a C2 frame's pass had 290 blocks (about one wave per SIMD) and was
+// latency-bound.
 // Each listed group's sphere mask goes to groupSel at the same list index:
 // the trace kernel takes it as the wave's primary-ray subset (one scalar
 // load) instead of recomputing the cull.
 // Heavy groups first (longest-processing-time order): the trace kernel's
-// waves take the list in order, and a launch ends with its last waves' tail
-// (a wave traces a whole pixel group; durations spread 3x around the
-// median), which dominates a short launch such as one GPU's shard of a
-// multi-GPU frame.  The groups are listed in four runs, heaviest first
-// (KernelArgs::groupCount):
+// waves take each partition's list in order (wave w: partition w % kListParts),
+// and a launch ends with its last waves' tail (a wave traces a whole pixel
+// group; durations spread 3x around the median), which dominates a short
+// launch such as one GPU's shard of a multi-GPU frame.  A partition's groups
+// are listed in four runs, heaviest first (KernelArgs::groupCount):
 //  * with launch-order feedback (a.groupCost: the previous launch of the same
 //    frame geometry wrote every listed group's trace time; a.costPrev: the
-//    sum and count of the times the previous cull pass read, whose mean is
+//    sums and counts of the times the previous cull pass read, whose mean is
 //    mu), by that time: >= 2 mu, >= mu, >= mu / 2, the rest.  A group's cost
 //    is a scheduling hint only: any value lists the group, so the frame is
 //    the same whatever the hint (a group dead last time reads a stale value).
 //    The pass also sums the times it reads into a.costStat, one atomic per
-//    block (the trace kernel's waves only store their group's time: 10^5
-//    atomics on one address from the trace waves cost a C3 frame 0.5 ms);
+//    block on its partition's sum (the trace kernel's waves only store their
+//    group's time: 10^5 atomics on one address from the trace waves cost a C3
+//    frame 0.5 ms);
 //  * otherwise (a geometry's first two launches, or feedback off) by the
 //    sphere mask: >= a.lptMin spheres first.
-// Run 0 fills the list's first half from the front, run 1 from its back,
-// runs 2 and 3 the second half likewise.
+// Partition p's region is [2 p cap, 2 (p + 1) cap) (cap = a.groupCap, the
+// groups of the partition's blocks): run 0 fills its first half from the
+// front, run 1 from the back, runs 2 and 3 the second half likewise.
+// One launch's counter sets: the run lengths and the cost sums of all list
+// partitions (KernelArgs::groupCount, costStat).
+constexpr size_t kCountSet = (size_t)kListParts * kCountStride;
+constexpr size_t kStatSet = (size_t)kListParts * kStatStride;
+
 template <unsigned kCullRounds>
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   __shared__ unsigned blockBase[4];
   __shared__ unsigned long long waveCost[4];
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const unsigned part = blockIdx.x % kListParts;
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned PPW = 64u / (nAA * nAA);
   const size_t total = (size_t)a.W * a.rowsLocal;
@@ -191,7 +204,9 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   // the previous launch's mean group time (ticks), 0: no feedback
   float mu = 0.f;
   if (a.costPrev != nullptr) {
-    const unsigned long long st = *a.costPrev;
+    unsigned long long st = 0;
+#pragma unroll
+    for (unsigned p = 0; p < kListParts; ++p) st += a.costPrev[p * kStatStride];
     const unsigned ng = (unsigned)(st >> 40);
     if (ng != 0u) mu = (float)(st & ((1ull << 40) - 1ull)) / (float)ng;
   }
@@ -204,6 +219,8 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     const unsigned pc = (unsigned)__builtin_popcountll(sel[k]);
     // Zero-fill the pixels of all this wave's groups with coalesced stores
     // (the trace kernel, later on the same stream, overwrites the live ones).
+    // Measured against writing only the empty groups from the trace kernel's
+    // first or last waves: as fast on C2, slower on C3 (profiles/r05/cull).
     const size_t wg0 = g - lane;  // the wave's first group this round
     if (wg0 < nGroups) {
       const size_t q0 = wg0 * PPW * 3;
@@ -240,13 +257,14 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     unsigned sum = 0;
     for (unsigned k = 0; k < kCullRounds; ++k)
       for (unsigned w = 0; w < 4; ++w) sum += cnt[c][k][w];
-    blockBase[c] = sum ? atomicAdd(&groupCount[c], sum) : 0u;
+    blockBase[c] = sum ? atomicAdd(&groupCount[part * kCountStride + c], sum) : 0u;
   } else if (threadIdx.x == 64 && a.costStat != nullptr) {
     const unsigned long long t = waveCost[0] + waveCost[1] + waveCost[2] + waveCost[3];
-    if (t) atomicAdd(a.costStat, t);
+    if (t) atomicAdd(a.costStat + part * kStatStride, t);
   }
   __syncthreads();
   const unsigned cap = a.groupCap;
+  const size_t region = (size_t)part * 2u * cap;
 #pragma unroll
   for (unsigned c = 0; c < 4; ++c) {
     unsigned off = blockBase[c];  // list order: (round, wave, lane)
@@ -260,8 +278,8 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
         const unsigned at = c == 0 ? r : c == 1 ? cap - 1u - r : c == 2 ? cap + r
                                                                        : 2u * cap - 1u - r;
-        groupList[at] = (unsigned)(blockG + k * 256 + threadIdx.x);
-        groupSel[at] = sel[k];
+        groupList[region + at] = (unsigned)(blockG + k * 256 + threadIdx.x);
+        groupSel[region + at] = sel[k];
       }
       for (unsigned w = wave; w < 4; ++w) off += cnt[c][k][w];
     }
@@ -302,7 +320,11 @@ struct rtg_context {
   uint4* timeline = nullptr;  // RTG_LAUNCH_TIMELINE records
   // Compacted-launch scratch: a ring of slots, so that renders of one
   // context on different streams can overlap; a slot is reused only after
-  // the event recorded behind its last trace kernel.
+  // the event recorded behind its last trace kernel (a wait skipped when that
+  // launch was on the same stream: stream order covers it).
+  // One event per launch, the slot's: created without the system-scope fence
+  // (hipEventDisableSystemFence), as it only orders this device's streams
+  // (a record with the fence wrote L2 back: ~2 us between launches on C2).
   // Its buffers are stream-ordered allocations (hipMallocAsync / hipFreeAsync
   // behind the slot's event), so growing them never blocks the host or other
   // streams.  count holds two sets of the four run lengths, used by
@@ -315,6 +337,7 @@ struct rtg_context {
     unsigned parity = 0;
     size_t cap = 0;
     hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;  // of its last launch
   };
   static constexpr int kSlots = 4;
   GroupSlot slots[kSlots];
@@ -324,8 +347,9 @@ struct rtg_context {
   // launches' sums; a few geometries at once (multi-GPU chunks render
   // different row sets in turn), least recently used replaced.
   // An entry's buffers are stream-ordered allocations too: a replaced entry's
-  // table is freed on the launching stream behind the event of its last
-  // launch (`done`), never with a device-wide synchronisation.
+  // table is freed on the launching stream behind its last launch, never with
+  // a device-wide synchronisation.  That launch's event is its slot's (`slot`):
+  // recorded again only by later launches, so waiting on it is conservative.
   struct CostEntry {
     unsigned long long key = 0;
     unsigned* cost = nullptr;
@@ -334,7 +358,8 @@ struct rtg_context {
     int cur = 0;
     unsigned launches = 0;
     unsigned long long lastUse = 0;
-    hipEvent_t done = nullptr;  // behind the entry's last trace kernel
+    int slot = -1;                 // the slot of its last launch
+    hipStream_t stream = nullptr;  // and that launch's stream
   };
   static constexpr int kCostEntries = 8;
   CostEntry costs[kCostEntries];
@@ -346,6 +371,7 @@ struct rtg_context {
   int lptMin = 2;        // heavy-first listing threshold (cull_groups_kernel; RTG_LPT_MIN A/B knob)
   size_t timelineCap = 0, timelineCount = 0;
   size_t lastGroups = 0;  // pixel groups of the last compacted launch (rtg_diag_group_list)
+  size_t lastPartCap = 0;  // and its list partitions' capacity (KernelArgs::groupCap)
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
   bool hasScene = false;
@@ -496,7 +522,6 @@ int rtg_context_destroy(rtg_context* ctx) {
   for (auto& ce : ctx->costs) {
     if (ce.cost) (void)hipFreeAsync(ce.cost, nullptr);
     if (ce.stat) (void)hipFreeAsync(ce.stat, nullptr);
-    if (ce.done) (void)hipEventDestroy(ce.done);
   }
   (void)hipStreamSynchronize(nullptr);
   delete ctx;
@@ -568,7 +593,6 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
     rtg_set_error("rtg_diag_group_list: no compacted launch yet");
     return RTG_ERR_INVALID;
   }
-  const size_t ng = slot.cap;  // the slot's capacity; the last launch's group count
   *groups = ctx->lastGroups;
   const size_t k = cap < ctx->lastGroups ? cap : ctx->lastGroups;
   HIP_TRY(hipSetDevice(ctx->device));
@@ -580,12 +604,46 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
     if (ce && ce->cap >= k) HIP_TRY(hipMemcpy(cost, ce->cost, k * sizeof(unsigned), hipMemcpyDeviceToHost));
     else memset(cost, 0, k * sizeof(unsigned));
   }
-  const size_t kl = 2 * k <= 2 * ng ? 2 * k : 2 * ng;
-  if (list) HIP_TRY(hipMemcpy(list, slot.list, kl * sizeof(unsigned), hipMemcpyDeviceToHost));
-  if (sel) HIP_TRY(hipMemcpy(sel, slot.sel, kl * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  if (runs)  // the set the last launch used (its trace kernel zeroed the other one)
-    HIP_TRY(hipMemcpy(runs, slot.count + 4 * (1 - slot.parity), 4 * sizeof(unsigned),
-                      hipMemcpyDeviceToHost));
+  if (!list && !sel && !runs) return RTG_OK;
+  // the set the last launch used (its trace kernel zeroed the other one)
+  std::vector<unsigned> cnt(kCountSet);
+  HIP_TRY(hipMemcpy(cnt.data(), slot.count + kCountSet * (1 - slot.parity),
+                    kCountSet * sizeof(unsigned), hipMemcpyDeviceToHost));
+  if (runs)
+    for (unsigned c = 0; c < 4; ++c) {
+      runs[c] = 0;
+      for (unsigned p = 0; p < kListParts; ++p) runs[c] += cnt[p * kCountStride + c];
+    }
+  if (!list && !sel) return RTG_OK;
+  std::vector<unsigned> l(slot.cap);
+  std::vector<unsigned long long> m(slot.cap);
+  HIP_TRY(hipMemcpy(l.data(), slot.list, slot.cap * sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(m.data(), slot.sel, slot.cap * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
+  // the trace kernel's order: index t is partition t % kListParts's
+  // run-order entry t / kListParts (trace_samples_body)
+  const size_t pc = ctx->lastPartCap;
+  size_t most = 0;
+  unsigned tot[kListParts];
+  for (unsigned p = 0; p < kListParts; ++p) {
+    const unsigned* g = &cnt[p * kCountStride];
+    tot[p] = g[0] + g[1] + g[2] + g[3];
+    if (tot[p] > most) most = tot[p];
+  }
+  size_t out = 0;
+  for (size_t t = 0; t < most * kListParts && out < k; ++t) {
+    const unsigned p = (unsigned)(t % kListParts);
+    const size_t j = t / kListParts;
+    if (j >= tot[p]) continue;
+    const unsigned* g = &cnt[p * kCountStride];
+    const size_t e0 = g[0], e1 = e0 + g[1], e2 = e1 + g[2];
+    const size_t r = j < e0 ? j : j < e1 ? pc - 1 - (j - e0) : j < e2 ? pc + (j - e1)
+                                                              : 2 * pc - 1 - (j - e2);
+    const size_t at = 2 * pc * p + r;
+    if (list) list[out] = l[at];
+    if (sel) sel[out] = m[at];
+    ++out;
+  }
   return RTG_OK;
 }
 
@@ -873,8 +931,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   unsigned threads = (unsigned)kBlock;
   dim3 grid((width + 15u) / 16u, (rows + 15u) / 16u);
   rtg_context::GroupSlot* slot = nullptr;  // compacted launch scratch
+  int slotIdx = -1;
   bool listed = false;                     // compacted launch (kList kernel)
   size_t cullGroups = 0;                   // pixel groups of the cull pass
+  unsigned cullRounds = 1;                 // its groups per lane
   if (sampleKernel) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
     const size_t groupsPerWave = variant == 21 ? 4 : 1;
@@ -893,28 +953,39 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     // groups no primary ray can leave (+0) and lists the others; a grid of
     // one-wave workgroups traces the listed groups round-robin.
     const bool compact = tpb == 64 && variant != 21 && variant != 22;
-    if (compact && ctx->n <= 64 && groups <= 0xFFFFFFFFull) {
+    // the cull pass's rounds per lane (cull_groups_kernel) and each list
+    // partition's capacity: the groups of its blocks
+    const size_t per4 = (size_t)256 * 4, minBlocks = (size_t)ctx->numCU * 4;
+    cullRounds = groups >= per4 * minBlocks ? 4u : groups >= per4 / 2 * minBlocks ? 2u : 1u;
+    const size_t cullBlocks = (groups + 256 * cullRounds - 1) / (256 * cullRounds);
+    const size_t partCap = (cullBlocks + kListParts - 1) / kListParts * 256 * cullRounds;
+    const size_t listCap = 2 * kListParts * partCap;  // list entries (KernelArgs::groupCap)
+    if (compact && ctx->n <= 64 && listCap < 0xFFFFFFFFull) {
       listed = true;
       const hipStream_t st = (hipStream_t)stream;
-      slot = &ctx->slots[ctx->nextSlot];
+      slotIdx = ctx->nextSlot;
+      slot = &ctx->slots[slotIdx];
       ctx->nextSlot = (ctx->nextSlot + 1) % rtg_context::kSlots;
-      if (!slot->done) HIP_TRY(hipEventCreateWithFlags(&slot->done, hipEventDisableTiming));
-      else HIP_TRY(hipStreamWaitEvent(st, slot->done, 0));  // the slot's last launch
-      if (slot->cap < groups) {
+      if (!slot->done)
+        HIP_TRY(hipEventCreateWithFlags(&slot->done,
+                                        hipEventDisableTiming | hipEventDisableSystemFence));
+      else if (slot->stream != st)
+        HIP_TRY(hipStreamWaitEvent(st, slot->done, 0));  // the slot's last launch
+      if (slot->cap < listCap) {
         // stream-ordered: freed after the slot's last kernel (waited on above)
         if (slot->list) HIP_TRY(hipFreeAsync(slot->list, st));
         if (slot->sel) HIP_TRY(hipFreeAsync(slot->sel, st));
         slot->list = nullptr;
         slot->sel = nullptr;
         slot->cap = 0;
-        // two halves of `groups` entries (the four runs, KernelArgs::groupCount)
-        HIP_TRY(hipMallocAsync((void**)&slot->list, 2 * groups * sizeof(unsigned), st));
-        HIP_TRY(hipMallocAsync((void**)&slot->sel, 2 * groups * sizeof(unsigned long long), st));
-        slot->cap = groups;
+        // the partitions' two halves (the four runs, KernelArgs::groupCount)
+        HIP_TRY(hipMallocAsync((void**)&slot->list, listCap * sizeof(unsigned), st));
+        HIP_TRY(hipMallocAsync((void**)&slot->sel, listCap * sizeof(unsigned long long), st));
+        slot->cap = listCap;
       }
       if (!slot->count) {
-        HIP_TRY(hipMallocAsync((void**)&slot->count, 8 * sizeof(unsigned), st));
-        HIP_TRY(hipMemsetAsync(slot->count, 0, 8 * sizeof(unsigned), st));
+        HIP_TRY(hipMallocAsync((void**)&slot->count, 2 * kCountSet * sizeof(unsigned), st));
+        HIP_TRY(hipMemsetAsync(slot->count, 0, 2 * kCountSet * sizeof(unsigned), st));
         slot->parity = 0;
       }
       if (ctx->orderFeedback && !(ctx->opts.flags & RTG_LAUNCH_NO_ORDER_FEEDBACK)) {
@@ -931,8 +1002,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
             if (e.lastUse < ce->lastUse) ce = &e;
           // the replaced entry's buffers may still be read by queued launches
           // (any stream): this stream waits for its last one
-          if (ce->done) HIP_TRY(hipStreamWaitEvent(st, ce->done, 0));
-          else HIP_TRY(hipEventCreateWithFlags(&ce->done, hipEventDisableTiming));
+          if (ce->slot >= 0 && ce->stream != st)
+            HIP_TRY(hipStreamWaitEvent(st, ctx->slots[ce->slot].done, 0));
           ce->key = 0;
           ce->launches = 0;
           if (ce->cap < groups) {
@@ -943,14 +1014,14 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
             ce->cap = groups;
           }
           if (!ce->stat)
-            HIP_TRY(hipMallocAsync((void**)&ce->stat, 2 * sizeof(unsigned long long), st));
-          HIP_TRY(hipMemsetAsync(ce->stat, 0, 2 * sizeof(unsigned long long), st));
+            HIP_TRY(hipMallocAsync((void**)&ce->stat, 2 * kStatSet * sizeof(unsigned long long), st));
+          HIP_TRY(hipMemsetAsync(ce->stat, 0, 2 * kStatSet * sizeof(unsigned long long), st));
           ce->cur = 0;
           ce->key = key;
         } else {
           // launches of this entry on other streams may still add to or zero
-          // its sums: this stream waits for the last one (a no-op on its own)
-          HIP_TRY(hipStreamWaitEvent(st, ce->done, 0));
+          // its sums: this stream waits for the last one
+          if (ce->stream != st) HIP_TRY(hipStreamWaitEvent(st, ctx->slots[ce->slot].done, 0));
         }
         // the trace kernel writes groupCost every launch; the cull pass reads
         // it (and sums it into costStat) once a launch has written it, and
@@ -958,11 +1029,11 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         // own state (cur, launches) advances only once nothing can fail
         // (commit below).
         a.groupCost = ce->cost;
-        a.costStat = ce->launches >= 1 ? ce->stat + ce->cur : nullptr;
-        a.costPrev = ce->launches >= 2 ? ce->stat + (1 - ce->cur) : nullptr;
+        a.costStat = ce->launches >= 1 ? ce->stat + kStatSet * ce->cur : nullptr;
+        a.costPrev = ce->launches >= 2 ? ce->stat + kStatSet * (1 - ce->cur) : nullptr;
         const unsigned nextCur = ce->launches >= 1 ? 1u - ce->cur : ce->cur;
         // the next launch's costStat, zeroed by this launch's trace kernel
-        a.zeroStat = ce->stat + nextCur;
+        a.zeroStat = ce->stat + kStatSet * nextCur;
         costEntry = ce;
       }
       cullGroups = groups;  // the cull pass is enqueued below, after the last failure point
@@ -974,11 +1045,14 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       if (ctx->persistPerCU > 0) persist = (size_t)ctx->numCU * ctx->persistPerCU;
       a.groupList = slot->list;
       a.groupSel = slot->sel;
-      a.groupCount = slot->count + 4 * slot->parity;
-      a.zeroCount = slot->count + 4 * (1 - slot->parity);  // parity flips at the commit
-      a.groupCap = (unsigned)groups;  // light groups are listed from index groups - 1 down
+      a.groupCount = slot->count + kCountSet * slot->parity;
+      a.zeroCount = slot->count + kCountSet * (1 - slot->parity);  // parity flips at the commit
+      a.groupCap = (unsigned)partCap;
       ctx->lastGroups = groups;
-      a.nPersist = (unsigned)(groups < persist ? groups : persist);
+      ctx->lastPartCap = partCap;
+      // a multiple of kListParts (wave w takes list partition w % kListParts)
+      const size_t np = groups < persist ? groups : persist;
+      a.nPersist = (unsigned)((np + kListParts - 1) / kListParts * kListParts);
       grid = dim3(a.nPersist, 1);
     }
   }
@@ -1017,6 +1091,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // this launch would have used).
   if (slot) slot->parity ^= 1u;
   if (costEntry) {
+    costEntry->slot = slotIdx;
+    costEntry->stream = (hipStream_t)stream;
     costEntry->lastUse = ++ctx->costClock;
     if (costEntry->launches >= 1) costEntry->cur = 1 - costEntry->cur;
     ++costEntry->launches;
@@ -1028,10 +1104,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // previous launch's trace kernel (KernelArgs::zeroCount / zeroStat).
   if (slot) {
     const hipStream_t st = (hipStream_t)stream;
-    const size_t per4 = (size_t)256 * 4, minBlocks = (size_t)ctx->numCU * 4;
-    const unsigned rounds = cullGroups >= per4 * minBlocks       ? 4u
-                            : cullGroups >= per4 / 2 * minBlocks ? 2u
-                                                                 : 1u;
+    const unsigned rounds = cullRounds;
     const dim3 cgrid((unsigned)((cullGroups + 256 * rounds - 1) / (256 * rounds)));
     unsigned* cnt = const_cast<unsigned*>(a.groupCount);
     if (rounds == 4)
@@ -1049,11 +1122,12 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       e = hipGetLastError();
     }
     if (e != hipSuccess) {  // no trace kernel zeroed the next launch's counters
-      (void)hipMemsetAsync(a.zeroCount, 0, 4 * sizeof(unsigned), st);
-      if (a.zeroStat) (void)hipMemsetAsync(a.zeroStat, 0, sizeof(unsigned long long), st);
+      (void)hipMemsetAsync(a.zeroCount, 0, kCountSet * sizeof(unsigned), st);
+      if (a.zeroStat)
+        (void)hipMemsetAsync(a.zeroStat, 0, kStatSet * sizeof(unsigned long long), st);
     }
-    (void)hipEventRecord(slot->done, st);  // on every path
-    if (costEntry) (void)hipEventRecord(costEntry->done, st);
+    (void)hipEventRecord(slot->done, st);  // on every path (the cost entry's too)
+    slot->stream = st;
     HIP_TRY(e);
     return RTG_OK;
   }

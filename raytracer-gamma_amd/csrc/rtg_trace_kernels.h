@@ -488,6 +488,14 @@ struct DevScene {
   }
 };
 
+// Compacted launch: the group list's partitions, each with its run counters
+// and cost sum on a 128-byte line of its own (cull_groups_kernel: device-scope
+// atomics on one address serialise).  A multiple of kListParts persistent
+// waves, so wave w always takes partition w % kListParts.
+constexpr unsigned kListParts = 16;
+constexpr unsigned kCountStride = 32;  // unsigned
+constexpr unsigned kStatStride = 16;   // unsigned long long
+
 struct KernelArgs;
 typedef void (*TraceFn)(const KernelArgs);
 
@@ -514,12 +522,13 @@ struct KernelArgs {
   // may hit, their count, and the number of persistent waves; null otherwise.
   const unsigned* groupList;
   const unsigned long long* groupSel;  // the listed groups' primary-ray sphere masks
-  // The list holds 2 x groupCap entries in four runs, read in this order:
-  // [0, count[0]) from the front of the first half, count[1] entries from its
-  // back (groupCap - 1 down), count[2] from the front of the second half and
-  // count[3] from its back (2 groupCap - 1 down); heaviest run first
-  // (cull_groups_kernel).
-  const unsigned* groupCount;  // [4] the runs' lengths
+  // The list has kListParts partitions of 2 x groupCap entries; partition p
+  // (at 2 p groupCap) holds four runs, read in this order: [0, count[0]) from
+  // the front of its first half, count[1] entries from its back (groupCap - 1
+  // down), count[2] from the front of the second half and count[3] from its
+  // back (2 groupCap - 1 down); heaviest run first (cull_groups_kernel).
+  // Partition p's run lengths are groupCount[p kCountStride + 0..3].
+  const unsigned* groupCount;
   unsigned groupCap;
   unsigned lptMin;             // cull_groups_kernel's popcount threshold (no cost feedback)
   unsigned nPersist;
@@ -529,11 +538,13 @@ struct KernelArgs {
   // geometry, which also sums what it reads (low 40 bits the ticks, high 24
   // the group count) for the launch after it.
   unsigned* groupCost;
+  // per list partition, at p kStatStride:
   unsigned long long* costStat;        // this cull pass's sums (zeroed before it), or null
   const unsigned long long* costPrev;  // the previous cull pass's, or null
   // Counters of the NEXT launch that this launch's trace kernel zeroes (its
-  // first wave, lane 0), so that no memset precedes a cull pass: the slot's
-  // other group-count set ([4]) and the cost entry's next costStat (or null).
+  // first wave, a lane per list partition), so that no memset precedes a cull
+  // pass: the slot's other group-count set and the cost entry's next costStat
+  // (or null).
   // Neither is in use while this launch's trace runs: the slot's previous
   // launch is complete (its event), and this launch's cull pass has read its
   // costPrev before the trace starts (one stream).
@@ -990,26 +1001,33 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
     const RTG_CONST unsigned* list = (const RTG_CONST unsigned*)a.groupList;
     // variant 24: the wave recomputes its primary cull (no cull-pass masks)
     const RTG_CONST unsigned long long* gsel = (const RTG_CONST unsigned long long*)a.groupSel;
-    // List position of run-order index idx (the four runs, heaviest first),
-    // or ~0u past the end; the run lengths are read afresh (scalar loads)
+    // List position of index idx: partition idx % kListParts (nPersist is a
+    // multiple of kListParts, so a wave stays in one partition), its run-order
+    // entry j = idx / kListParts (the four runs, heaviest first), or ~0u past
+    // the partition's end; the run lengths are read afresh (scalar loads)
     // rather than held in SGPRs through the trace.
     auto pos = [](unsigned idx) {
+      const unsigned part = idx % kListParts, j = idx / kListParts;
       const RTG_CONST KernelArgs* b = kargs();
-      const RTG_CONST unsigned* gc = (const RTG_CONST unsigned*)b->groupCount;
+      const RTG_CONST unsigned* gc =
+          (const RTG_CONST unsigned*)b->groupCount + part * kCountStride;
       const unsigned cap = b->groupCap;
       const unsigned e0 = gc[0], e1 = e0 + gc[1], e2 = e1 + gc[2], e3 = e2 + gc[3];
-      return idx < e0 ? idx
-           : idx < e1 ? cap - 1u - (idx - e0)
-           : idx < e2 ? cap + (idx - e1)
-           : idx < e3 ? 2u * cap - 1u - (idx - e2)
-                      : ~0u;
+      const unsigned r = j < e0 ? j
+                       : j < e1 ? cap - 1u - (j - e0)
+                       : j < e2 ? cap + (j - e1)
+                       : j < e3 ? 2u * cap - 1u - (j - e2)
+                                : ~0u;
+      return r == ~0u ? r : 2u * cap * part + r;
     };
     record_wave_start(a, t0, gw);
-    if (gw == 0 && (threadIdx.x & 63u) == 0) {  // the next launch's counters (KernelArgs)
+    if (gw == 0) {  // the next launch's counters (KernelArgs), lane p: partition p's
       const RTG_CONST KernelArgs* b = kargs();
-      unsigned* zc = b->zeroCount;
-      zc[0] = zc[1] = zc[2] = zc[3] = 0u;
-      if (unsigned long long* zs = b->zeroStat) *zs = 0ull;
+      const unsigned l = threadIdx.x & 63u;
+      if (l < kListParts) {
+        *(uint4*)(b->zeroCount + l * kCountStride) = make_uint4(0u, 0u, 0u, 0u);
+        if (unsigned long long* zs = b->zeroStat) zs[l * kStatStride] = 0ull;
+      }
     }
     unsigned tg = t0;  // this group's start (the first one's includes the wave's set-up)
     for (unsigned idx = (unsigned)gw;; idx += kargs()->nPersist) {

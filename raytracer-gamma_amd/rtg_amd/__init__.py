@@ -425,22 +425,24 @@ class Context:
         return out[:min(cap, cnt.value)]
 
     def diag_group_list(self, cap: int = 1 << 26):
-        """The last compacted launch: {cost[groups], list[2 groups], sel[2 groups],
-        runs[4]} (rtg_diag_group_list; costs in 100 MHz ticks)."""
+        """The last compacted launch: {cost[groups], list[listed], sel[listed],
+        runs[4]}, list and sel in the trace kernel's order (rtg_diag_group_list;
+        costs in 100 MHz ticks)."""
         n = ctypes.c_size_t(0)
         _check(lib().rtg_diag_group_list(self._h, None, None, None, None, 0, ctypes.byref(n)),
                "rtg_diag_group_list")
         g = min(cap, n.value)
         cost = np.zeros(g, np.uint32)
-        lst = np.zeros(2 * g, np.uint32)
-        sel = np.zeros(2 * g, np.uint64)
+        lst = np.zeros(g, np.uint32)
+        sel = np.zeros(g, np.uint64)
         runs = np.zeros(4, np.uint32)
         _check(lib().rtg_diag_group_list(self._h, ctypes.c_void_p(cost.ctypes.data),
                                          ctypes.c_void_p(lst.ctypes.data),
                                          ctypes.c_void_p(sel.ctypes.data),
                                          ctypes.c_void_p(runs.ctypes.data), g, ctypes.byref(n)),
                "rtg_diag_group_list")
-        return {"cost": cost, "list": lst, "sel": sel, "runs": runs}
+        k = int(runs.sum())
+        return {"cost": cost, "list": lst[:k], "sel": sel[:k], "runs": runs}
 
     def render_device(self, width, height, dst_ptr: int, zoom=-4.0, alias_factor=3.0,
                       stack_size=6, row_block=16, shard=0, n_shards=1, stream: int = 0):

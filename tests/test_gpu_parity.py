@@ -388,6 +388,38 @@ def test_failed_launch_leaves_slots_consistent(R, golden, torch_cuda):
     ctx.close()
 
 
+def test_group_list_partitions(R, golden, torch_cuda):
+    """The compacted launch's list (cull_groups_kernel: kListParts partitions,
+    each with its own run counters): over a cold launch, a launch whose cull
+    pass sums the cost table and a launch ordered by it, every listed group
+    appears once, has a non-empty sphere mask, and every group with a non-zero
+    pixel is listed (the others were zero-filled by the cull pass)."""
+    torch = torch_cuda
+    c = golden["configs"]["c2"]
+    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    W, H, S = c["W"], c["H"], c["stack_size"]
+    ctx = R.Context(0)
+    ctx.set_scene(sph, lg)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    ppw = 64 // 9
+    groups = (W * H + ppw - 1) // ppw
+    for launch in range(3):
+        out.fill_(5.0)
+        ctx.render_device(W, H, out.data_ptr(), stack_size=S, stream=stream)
+        torch.cuda.synchronize()
+        assert canon_md5(out.cpu().numpy()) == c["fb_md5"]
+        d = ctx.diag_group_list()
+        lst = d["list"].astype(np.int64)
+        assert len(lst) == int(d["runs"].sum()) > 0
+        assert len(np.unique(lst)) == len(lst) and lst.max() < groups
+        assert (d["sel"] != 0).all()
+        px = (out.cpu().numpy().reshape(-1, 3) != 0).any(axis=1)
+        lit = np.unique(np.nonzero(px)[0] // ppw)
+        assert np.isin(lit, lst).all(), launch
+    ctx.close()
+
+
 @pytest.mark.parametrize("variant", [0, 9])
 def test_variant_full_frames(R, golden, torch_cuda, variant):
     """Kernel mappings over whole frames, sharded frames, row lists and

@@ -56,14 +56,9 @@ def dump(cfg, out, reps):
 
 
 def listed(d):
-    """(group, sel) of every listed group, in list order (runs 0..3)."""
-    lst, sel, runs = d["list"], d["sel"], d["runs"]
-    cap = len(lst) // 2
-    e = [int(x) for x in runs]
-    idx = list(range(e[0])) + [cap - 1 - k for k in range(e[1])] + \
-        [cap + k for k in range(e[2])] + [2 * cap - 1 - k for k in range(e[3])]
-    idx = np.array(idx, np.int64)
-    return lst[idx].astype(np.int64), sel[idx]
+    """(group, sel) of every listed group, in the trace kernel's order."""
+    n = int(d["runs"].sum())
+    return d["list"][:n].astype(np.int64), d["sel"][:n]
 
 
 def makespan(costs, slots):
