@@ -148,16 +148,20 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
   return sel;
 }
 
-// A block takes R x 256 consecutive groups (one per lane per round) and
-// appends its live ones with one atomic per run, in one of kListParts list
-// partitions (block b: partition b % kListParts), each with its own run
-// counters and cost sum on a cache line of its own.  Device-scope atomics on
-// one address serialise (tools/cull_micro.hip, 1158 workgroups: one address
-// 15.1 us, 8 lines 4.5, 32 lines 3.7, no atomic 3.7): with the whole list on
-// one set of counters the C2 pass took 21 us, 11 of them queued atomics.
-// R (the launch picks 1, 2 or 4) keeps at least ~4 blocks per CU: with R = 4
-// a C2 frame's pass had 290 blocks (about one wave per SIMD) and was
-// latency-bound.
+// One launch's counter sets: the run lengths and the cost sums of all list
+// partitions (KernelArgs::groupCount, costStat).
+constexpr size_t kCountSet = (size_t)kListParts * kCountStride;
+constexpr size_t kStatSet = (size_t)kListParts * kStatStride;
+
+// A block takes 256 consecutive groups (one per lane) and appends its live
+// ones with one atomic per run, in one of kListParts list partitions (block
+// b: partition b % kListParts), each with its own run counters and cost sum
+// on a cache line of its own.  Device-scope atomics on one address serialise
+// (tools/cull_micro.hip, 1158 workgroups: one address 15.1 us, 8 lines 4.5,
+// 32 lines 3.7, no atomic 3.7): with the whole list on one set of counters
+// the C2 pass took 21 us, 11 of them queued atomics.  Once they no longer
+// queue, one group per lane beats the 2 or 4 per lane that had kept the
+// block count down (C3 pass 39 -> 31 us, C4 frame -1 %).
 // Each listed group's sphere mask goes to groupSel at the same list index:
 // the trace kernel takes it as the wave's primary-ray subset (one scalar
 // load) instead of recomputing the cull.
@@ -182,17 +186,11 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
 // Partition p's region is [2 p cap, 2 (p + 1) cap) (cap = a.groupCap, the
 // groups of the partition's blocks): run 0 fills its first half from the
 // front, run 1 from the back, runs 2 and 3 the second half likewise.
-// One launch's counter sets: the run lengths and the cost sums of all list
-// partitions (KernelArgs::groupCount, costStat).
-constexpr size_t kCountSet = (size_t)kListParts * kCountStride;
-constexpr size_t kStatSet = (size_t)kListParts * kStatStride;
-
-template <unsigned kCullRounds>
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
                                                           unsigned long long* groupSel,
                                                           unsigned* groupCount) {
-  __shared__ unsigned cnt[4][kCullRounds][4];
+  __shared__ unsigned cnt[4][4];
   __shared__ unsigned blockBase[4];
   __shared__ unsigned long long waveCost[4];
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -200,7 +198,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   const unsigned nAA = (unsigned)a.cam.nAA;
   const unsigned PPW = 64u / (nAA * nAA);
   const size_t total = (size_t)a.W * a.rowsLocal;
-  const size_t blockG = (size_t)blockIdx.x * (256 * kCullRounds);
+  const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
   // the previous launch's mean group time (ticks), 0: no feedback
   float mu = 0.f;
   if (a.costPrev != nullptr) {
@@ -210,41 +208,37 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     const unsigned ng = (unsigned)(st >> 40);
     if (ng != 0u) mu = (float)(st & ((1ull << 40) - 1ull)) / (float)ng;
   }
-  uint64_t live[4][kCullRounds], sel[kCullRounds];
-  unsigned long long costAcc = 0;  // this lane's listed groups: time sum (low 40), count
+  const uint64_t sel = g < nGroups ? group_sel(a, g, PPW, total) : 0ull;
+  const unsigned pc = (unsigned)__builtin_popcountll(sel);
+  // Zero-fill the pixels of all this wave's groups with coalesced stores
+  // (the trace kernel, later on the same stream, overwrites the live ones).
+  // Measured against writing only the empty groups from the trace kernel's
+  // first or last waves: as fast on C2, slower on C3 (profiles/r05/cull).
+  const size_t wg0 = g - lane;  // the wave's first group
+  if (wg0 < nGroups) {
+    const size_t q0 = wg0 * PPW * 3;
+    size_t q1 = (wg0 + 64) * PPW * 3;
+    if (q1 > total * 3) q1 = total * 3;
+    for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
+  }
+  unsigned cost = 0;
+  unsigned long long costAcc = 0;  // this lane's listed group: time (low 40), count
+  if (a.costStat != nullptr && a.groupCost != nullptr && pc != 0u) {
+    cost = a.groupCost[g];
+    costAcc = (1ull << 40) | (unsigned long long)cost;
+  }
+  unsigned run;
+  if (mu > 0.f) {
+    const float c = (float)cost;
+    run = c >= 2.f * mu ? 0u : c >= mu ? 1u : c >= 0.5f * mu ? 2u : 3u;
+  } else {
+    run = pc >= a.lptMin ? 0u : 1u;
+  }
+  uint64_t live[4];
 #pragma unroll
-  for (unsigned k = 0; k < kCullRounds; ++k) {
-    const size_t g = blockG + k * 256 + threadIdx.x;
-    sel[k] = g < nGroups ? group_sel(a, g, PPW, total) : 0ull;
-    const unsigned pc = (unsigned)__builtin_popcountll(sel[k]);
-    // Zero-fill the pixels of all this wave's groups with coalesced stores
-    // (the trace kernel, later on the same stream, overwrites the live ones).
-    // Measured against writing only the empty groups from the trace kernel's
-    // first or last waves: as fast on C2, slower on C3 (profiles/r05/cull).
-    const size_t wg0 = g - lane;  // the wave's first group this round
-    if (wg0 < nGroups) {
-      const size_t q0 = wg0 * PPW * 3;
-      size_t q1 = (wg0 + 64) * PPW * 3;
-      if (q1 > total * 3) q1 = total * 3;
-      for (size_t q = q0 + lane; q < q1; q += 64) a.dst[q] = 0.f;
-    }
-    unsigned cost = 0;
-    if (a.costStat != nullptr && a.groupCost != nullptr && pc != 0u) {
-      cost = a.groupCost[g];
-      costAcc += (1ull << 40) | (unsigned long long)cost;
-    }
-    unsigned run;
-    if (mu > 0.f) {
-      const float c = (float)cost;
-      run = c >= 2.f * mu ? 0u : c >= mu ? 1u : c >= 0.5f * mu ? 2u : 3u;
-    } else {
-      run = pc >= a.lptMin ? 0u : 1u;
-    }
-#pragma unroll
-    for (unsigned c = 0; c < 4; ++c) {
-      live[c][k] = __ballot(pc != 0u && run == c);
-      if (lane == 0) cnt[c][k][wave] = (unsigned)__builtin_popcountll(live[c][k]);
-    }
+  for (unsigned c = 0; c < 4; ++c) {
+    live[c] = __ballot(pc != 0u && run == c);
+    if (lane == 0) cnt[c][wave] = (unsigned)__builtin_popcountll(live[c]);
   }
   if (a.costStat != nullptr) {  // the wave's sum (butterfly), for this launch's stat
 #pragma unroll
@@ -254,9 +248,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   __syncthreads();
   if (threadIdx.x < 4) {
     const unsigned c = threadIdx.x;
-    unsigned sum = 0;
-    for (unsigned k = 0; k < kCullRounds; ++k)
-      for (unsigned w = 0; w < 4; ++w) sum += cnt[c][k][w];
+    const unsigned sum = cnt[c][0] + cnt[c][1] + cnt[c][2] + cnt[c][3];
     blockBase[c] = sum ? atomicAdd(&groupCount[part * kCountStride + c], sum) : 0u;
   } else if (threadIdx.x == 64 && a.costStat != nullptr) {
     const unsigned long long t = waveCost[0] + waveCost[1] + waveCost[2] + waveCost[3];
@@ -267,21 +259,15 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   const size_t region = (size_t)part * 2u * cap;
 #pragma unroll
   for (unsigned c = 0; c < 4; ++c) {
-    unsigned off = blockBase[c];  // list order: (round, wave, lane)
-#pragma unroll
-    for (unsigned k = 0; k < kCullRounds; ++k) {
-      for (unsigned w = 0; w < 4; ++w)
-        if (w < wave) off += cnt[c][k][w];
-      const uint64_t m = live[c][k];
-      if ((m >> lane) & 1ull) {
-        const unsigned r = off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        const unsigned at = c == 0 ? r : c == 1 ? cap - 1u - r : c == 2 ? cap + r
-                                                                       : 2u * cap - 1u - r;
-        groupList[region + at] = (unsigned)(blockG + k * 256 + threadIdx.x);
-        groupSel[region + at] = sel[k];
-      }
-      for (unsigned w = wave; w < 4; ++w) off += cnt[c][k][w];
+    const uint64_t m = live[c];
+    if ((m >> lane) & 1ull) {
+      unsigned off = blockBase[c];  // list order: (wave, lane)
+      for (unsigned w = 0; w < wave; ++w) off += cnt[c][w];
+      const unsigned r = off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      const unsigned at = c == 0 ? r : c == 1 ? cap - 1u - r : c == 2 ? cap + r : 2u * cap - 1u - r;
+      groupList[region + at] = (unsigned)g;
+      groupSel[region + at] = sel;
     }
   }
 }
@@ -934,7 +920,6 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   int slotIdx = -1;
   bool listed = false;                     // compacted launch (kList kernel)
   size_t cullGroups = 0;                   // pixel groups of the cull pass
-  unsigned cullRounds = 1;                 // its groups per lane
   if (sampleKernel) {
     const unsigned ppw = 64u / (unsigned)(a.cam.nAA * a.cam.nAA);  // >= 1: nAA <= 8 here
     const size_t groupsPerWave = variant == 21 ? 4 : 1;
@@ -953,12 +938,9 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     // groups no primary ray can leave (+0) and lists the others; a grid of
     // one-wave workgroups traces the listed groups round-robin.
     const bool compact = tpb == 64 && variant != 21 && variant != 22;
-    // the cull pass's rounds per lane (cull_groups_kernel) and each list
-    // partition's capacity: the groups of its blocks
-    const size_t per4 = (size_t)256 * 4, minBlocks = (size_t)ctx->numCU * 4;
-    cullRounds = groups >= per4 * minBlocks ? 4u : groups >= per4 / 2 * minBlocks ? 2u : 1u;
-    const size_t cullBlocks = (groups + 256 * cullRounds - 1) / (256 * cullRounds);
-    const size_t partCap = (cullBlocks + kListParts - 1) / kListParts * 256 * cullRounds;
+    // each list partition's capacity: the groups of its cull-pass blocks
+    const size_t cullBlocks = (groups + 255) / 256;
+    const size_t partCap = (cullBlocks + kListParts - 1) / kListParts * 256;
     const size_t listCap = 2 * kListParts * partCap;  // list entries (KernelArgs::groupCap)
     if (compact && ctx->n <= 64 && listCap < 0xFFFFFFFFull) {
       listed = true;
@@ -1104,18 +1086,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // previous launch's trace kernel (KernelArgs::zeroCount / zeroStat).
   if (slot) {
     const hipStream_t st = (hipStream_t)stream;
-    const unsigned rounds = cullRounds;
-    const dim3 cgrid((unsigned)((cullGroups + 256 * rounds - 1) / (256 * rounds)));
+    const dim3 cgrid((unsigned)((cullGroups + 255) / 256));
     unsigned* cnt = const_cast<unsigned*>(a.groupCount);
-    if (rounds == 4)
-      hipLaunchKernelGGL(cull_groups_kernel<4>, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
-                         slot->sel, cnt);
-    else if (rounds == 2)
-      hipLaunchKernelGGL(cull_groups_kernel<2>, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
-                         slot->sel, cnt);
-    else
-      hipLaunchKernelGGL(cull_groups_kernel<1>, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
-                         slot->sel, cnt);
+    hipLaunchKernelGGL(cull_groups_kernel, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
+                       slot->sel, cnt);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
       hipLaunchKernelGGL(fn, grid, dim3(threads), lds, st, a);
