@@ -105,48 +105,50 @@ UNIT_COST = {
 }
 
 # Round 5: the unit prices above fitted to the hardware's SQ_INSTS_VALU over 29
-# scenes of both kernel kinds (the bench configs at reduced frames weighted
-# 4x, seeded masked and BVH scenes; a ridge toward the source prices, bounds
-# 0.6-1.7x): tools/calib_units.py, data and fit in profiles/r05/calib_units*.
-# rms model/PMC error 7.6 % -> 3.3 % over the set; C3 1.035 -> 1.019, C5
-# 1.017 -> 1.011.  The prices a unit's source gives stay documented above;
-# these are the ones the bench line uses.
+# scenes of both kernel kinds (tools/calib_units.py: the bench configs C1-C5,
+# C2 and C3 at full size, weighted 10x, then seeded masked and BVH scenes; a
+# ridge toward the previous prices, bounds 0.6-1.7x of them), refitted on the
+# final round-5 sources: rms model/PMC error over the set 6.9 % -> 2.8 %; C2
+# 1.027 -> 1.001, C3 1.026 -> 1.000, C4 1.005 -> 0.999, C5 (a quarter of each
+# side) 0.938 -> 1.002 (profiles/r05/calib_units_final*; the first fit, on
+# reduced frames: profiles/r05/calib_units*).  The prices a unit's source gives
+# stay documented above; these are the ones the bench line uses.
 UNIT_COST_SOURCE = dict(UNIT_COST)
 UNIT_COST.update({
-    "U.query": 17.64,
-    "U.primIter": 11.52,
-    "U.primExact": 46.85,
-    "U.selIter": 9.44,
-    "U.selExact": 40.52,
-    "U.shdIter": 11.07,
-    "U.shdExact": 53.34,
-    "U.enterHead": 76.61,
-    "U.enterIter": 2.95,
-    "U.enterExact": 42.18,
-    "U.fullGroup": 51.74,
-    "U.fullExact": 74.26,
-    "U.bvhNode": 2.0,
-    "U.bvhSlot": 20.25,
-    "U.bvhExact": 56.3,
-    "U.contIter": 12.32,
-    "U.contBvhNode": 45.68,
-    "U.cone": 16.07,
-    "U.maskIter": 4.02,
-    "U.node": 13.43,
-    "U.shade": 79.89,
-    "U.light": 10.3,
-    "U.lightDir": 28.64,
-    "U.shadow": 2.97,
-    "U.lit": 15.86,
-    "U.refr": 204.53,
-    "U.refrLeaf": 285.46,
-    "U.push": 49.51,
-    "U.descend": 27.48,
-    "U.unwind": 11.8,
-    "U.capIter": 14.31,
-    "U.ovIter": 14.64,
-    "U.sample": 136.0,
-    "U.wave": 30.96,
+    "U.query": 18.29,
+    "U.primIter": 11.4,
+    "U.primExact": 45.91,
+    "U.selIter": 9.38,
+    "U.selExact": 38.64,
+    "U.shdIter": 9.98,
+    "U.shdExact": 49.99,
+    "U.enterHead": 70.1,
+    "U.enterIter": 2.94,
+    "U.enterExact": 35.53,
+    "U.fullGroup": 50.37,
+    "U.fullExact": 90.87,
+    "U.bvhNode": 2.02,
+    "U.bvhSlot": 27.99,
+    "U.bvhExact": 53.0,
+    "U.contIter": 11.79,
+    "U.contBvhNode": 44.6,
+    "U.cone": 15.7,
+    "U.maskIter": 3.99,
+    "U.node": 13.6,
+    "U.shade": 86.68,
+    "U.light": 10.4,
+    "U.lightDir": 31.04,
+    "U.shadow": 2.98,
+    "U.lit": 16.0,
+    "U.refr": 180.32,
+    "U.refrLeaf": 259.41,
+    "U.push": 49.63,
+    "U.descend": 27.09,
+    "U.unwind": 11.72,
+    "U.capIter": 13.25,
+    "U.ovIter": 11.34,
+    "U.sample": 159.59,
+    "U.wave": 30.15,
 })
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # one wave64 VALU op per 2 cycles per SIMD
