@@ -916,7 +916,8 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         const int h0 = sc.lane_with(enterH, todo);
         if (todo && enterH == h0) {
           bool ok;
-          const int hh = closest_enter_list(sc, q, h0, t, ok);
+          // scalar h0 (blocked_cap_lanes)
+          const int hh = closest_enter_list(sc, q, sc.first_lane_i(h0), t, ok);
           if (sc.all(ok)) {
             hit = hh;
             done = true;
@@ -1705,7 +1706,10 @@ RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l
   for (int k = 0; k < kListWalks; ++k) {  // wave-uniform
     const int h0 = sc.lane_with(h, todo);
     if (todo && h == h0) {
-      blk = blocked_cap(sc, o, d, gap, l, h0);
+      // h0 made scalar again inside the branch: the compiler otherwise
+      // substitutes the lane's own h (equal here, but a VGPR) and the walk's
+      // range and record loads become per-lane vector loads
+      blk = blocked_cap(sc, o, d, gap, l, sc.first_lane_i(h0));
       todo = false;
     }
     if (!sc.any(todo)) return blk;
@@ -1720,7 +1724,7 @@ RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT) {
   for (int k = 0; k < kListWalks; ++k) {  // wave-uniform
     const int h0 = sc.lane_with(h, todo);
     if (todo && h == h0) {
-      found = container_list(sc, pt, h0, nT);
+      found = container_list(sc, pt, sc.first_lane_i(h0), nT);  // scalar h0 (above)
       todo = false;
     }
     if (!sc.any(todo)) return found;
