@@ -592,7 +592,10 @@ template <class Scene>
 RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut);
 // Most distinct spheres a wave walks the per-sphere lists of (blocked_cap_lanes
 // and friends) before its remaining lanes take the BVH.
-constexpr int kListWalks = 5;
+#ifndef RTG_LIST_WALKS  // A/B builds only (tools/ab_build.sh EXTRA=-DRTG_LIST_WALKS=N)
+#define RTG_LIST_WALKS 5
+#endif
+constexpr int kListWalks = RTG_LIST_WALKS;
 template <class Scene>
 RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
