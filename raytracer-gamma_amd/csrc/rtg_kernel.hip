@@ -742,7 +742,7 @@ int rtg_context_set_scene(rtg_context* ctx, const rtg_sphere* spheres, unsigned 
                       hipMemcpyHostToDevice));
   }
   if (!ps.capOff.empty()) {
-    if (hipMalloc(&ctx->capRec, (ps.capRec.size() + kListWords) * sizeof(float)) != hipSuccess ||
+    if (hipMalloc(&ctx->capRec, (ps.capRec.size() + 4 * kCapWords) * sizeof(float)) != hipSuccess ||
         hipMalloc(&ctx->capOff, ps.capOff.size() * sizeof(unsigned)) != hipSuccess ||
         hipMalloc(&ctx->ovRec, (ps.ovRec.size() + kListWords) * sizeof(float)) != hipSuccess ||
         hipMalloc(&ctx->ovOff, ps.ovOff.size() * sizeof(unsigned)) != hipSuccess) {

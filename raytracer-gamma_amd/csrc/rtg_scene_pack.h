@@ -284,6 +284,9 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
 // kListMaxTests get no lists.  Either way the tables stay empty, has_lists()
 // is false and every query takes the BVH (same answers, slower).
 constexpr int kListWords = 8;
+// records read past a list's end by one load: padding at each table's end
+constexpr int kCapPad = 64 / (4 * kCapWords) - 1;
+constexpr int kOvPad = 1;
 constexpr size_t kListMaxRecords = size_t(1) << 23;
 constexpr double kListMaxTests = 0x1p28;
 inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
@@ -340,7 +343,7 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
   for (auto& th : pool) th.join();
   size_t capTotal = 0;
   for (const auto& l : lists) capTotal += l.size();
-  if (capTotal + 1 > maxRecords) return;  // (+1: the padding record)
+  if (capTotal + kCapPad > maxRecords) return;  // (the padding records)
   std::vector<std::vector<unsigned>> ov(n);
   size_t ovTotal = 0;
   for (unsigned h = 0; h < n; ++h) {
@@ -349,11 +352,19 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
     ovTotal += ov[h].size();
     if (ovTotal + 1 > maxRecords) return;
   }
-  ps->capRec.reserve((capTotal + 1) * kListWords);
+  ps->capRec.reserve((capTotal + kCapPad) * kCapWords);
   ps->capOff.push_back(0);
   for (unsigned q = 0; q < total; ++q) {
-    for (unsigned i : lists[q]) rec(ps->capRec, i);
-    ps->capOff.push_back((unsigned)(ps->capRec.size() / kListWords));
+    for (unsigned i : lists[q]) {
+      if (kCapWords == kListWords) {
+        rec(ps->capRec, i);
+      } else {
+        const rtg_sphere& sp = spheres[i];
+        const float w[4] = {sp.pos.x, sp.pos.y, sp.pos.z, sp.radius * sp.radius};  // raytracer.h:100
+        ps->capRec.insert(ps->capRec.end(), w, w + 4);
+      }
+    }
+    ps->capOff.push_back((unsigned)(ps->capRec.size() / kCapWords));
   }
   ps->ovRec.reserve((ovTotal + 1) * kListWords);
   ps->ovOff.push_back(0);
@@ -361,11 +372,13 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
     for (unsigned j : ov[h]) rec(ps->ovRec, j);
     ps->ovOff.push_back((unsigned)(ps->ovRec.size() / kListWords));
   }
-  // one padding record past each table's end: the kernel reads records in
-  // pairs (one 64-byte scalar load) and ignores the second past a list's end
+  // padding records past each table's end: the kernel reads a 64-byte
+  // scalar load of records at a time (two overlap records, four capsule
+  // records) and the ones past a list's end are the next list's or these,
+  // whose NaN centres accept no root
   const float pad[kListWords] = {NAN, NAN, NAN, NAN, NAN, NAN, 0.f, 1.f};
-  ps->capRec.insert(ps->capRec.end(), pad, pad + kListWords);
-  ps->ovRec.insert(ps->ovRec.end(), pad, pad + kListWords);
+  for (int k = 0; k < kCapPad; ++k) ps->capRec.insert(ps->capRec.end(), pad, pad + kCapWords);
+  for (int k = 0; k < kOvPad; ++k) ps->ovRec.insert(ps->ovRec.end(), pad, pad + kListWords);
 }
 
 inline float round_up_f(double v) {

@@ -1364,6 +1364,27 @@ struct ListRec {
   float rs, r2, cr, rf;
   int idx;
 };
+// Capsule-list records (sphere_lists, rtg_scene_pack.h): RTG_CAP_WORDS = 4 (the
+// default) {x, y, z, r^2}, four to a 64-byte scalar load, the screen radius^2
+// derived on the device (cap_screen_r2); RTG_CAP_WORDS = 8 (A/B builds) the
+// overlap lists' 32-byte records, two to a load.
+#ifndef RTG_CAP_WORDS
+#define RTG_CAP_WORDS 4
+#endif
+constexpr int kCapWords = RTG_CAP_WORDS;
+// One capsule-list record (16-byte form, kCapWords == 4): centre and r^2.
+struct CapRec {
+  V3 c;
+  float r2;
+};
+// The pass-1 screen radius^2 of a 16-byte capsule record, on the device: any
+// rs >= r^2 (1 + 2K + 4K^2) keeps pass1_rad's screen conservative (screen_r2
+// rounds that up on the host); fma(r2, C, 2^-149) with C = (1 + 2K + 4K^2)
+// (1 + 2^-22) rounded up is at least that for every r2 >= 0 (normal results
+// lose under 2^-24 relative, subnormal ones under 2^-150, which the 2^-149
+// covers), and NaN / inf stay NaN / inf.  A larger rs only lets more
+// spheres through to the exact test, so the answer is the same.
+RTG_HD float cap_screen_r2(float r2) { return fmaf(r2, 0x1.000206p+0f, 0x1p-149f); }
 struct BvhRec {
   float s[24];
   int ch[4];
@@ -1606,6 +1627,25 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
       take_blocker(t, q.d, gap, blk);
     }
   };
+#if RTG_CAP_WORDS == 4
+  // four 16-byte records per 64-byte scalar load; those past the list's end
+  // are the next list's (or the table's padding): a real sphere can only
+  // block if it blocks, so testing it keeps the answer; one exit test per
+  // load
+  for (unsigned k = k0; k < k1; k += 4) {  // wave-uniform
+    CapRec r[4];
+    sc.cap_rec4(k, r);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ListRec e;
+      e.c = r[j].c;
+      e.r2 = r[j].r2;
+      e.rs = cap_screen_r2(r[j].r2);
+      step(e);
+    }
+    if (sc.all(blk)) break;
+  }
+#else
   for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
     ListRec r0, r1;
     sc.cap_rec2(k, r0, r1);
@@ -1617,6 +1657,7 @@ RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int 
     step(r1);
     if (sc.all(blk)) break;
   }
+#endif
   return blk;
 }
 

@@ -287,12 +287,18 @@ struct DevScene {
   __device__ __forceinline__ void cap_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
     list_rec2(capRec, k, r0, r1);
   }
+  // Capsule records k .. k + 3 (16-byte form) with one 64-byte scalar load.
+  __device__ __forceinline__ void cap_rec4(unsigned k, CapRec* r) const {
+    typedef float f16 __attribute__((ext_vector_type(16)));
+    const f16 g = *(const RTG_CONST f16*)fidx(capRec, 4u * k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r[j].c = v3(g[4 * j], g[4 * j + 1], g[4 * j + 2]);
+      r[j].r2 = g[4 * j + 3];
+    }
+  }
   __device__ __forceinline__ void ov_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
-  }
-  __device__ __forceinline__ V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
-                                        float& rf) const {
-    return list_rec(capRec, k, rs, r2, cr, idx, rf);
   }
   __device__ __forceinline__ V3 ov_rec(unsigned k, float& rs, float& r2, float& cr, int& idx,
                                        float& rf) const {

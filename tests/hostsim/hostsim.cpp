@@ -61,11 +61,15 @@ struct HostScene {
   void cap_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
     list_rec2(capRec, k, r0, r1);
   }
+  void cap_rec4(unsigned k, rtg::CapRec* r) const {
+    for (int j = 0; j < 4; ++j) {
+      const float* g = capRec + 4 * ((size_t)k + j);
+      r[j].c = rtg::v3(g[0], g[1], g[2]);
+      r[j].r2 = g[3];
+    }
+  }
   void ov_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
-  }
-  rtg::V3 cap_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
-    return list_rec(capRec, k, rs, r2, cr, idx, rf);
   }
   rtg::V3 ov_rec(unsigned k, float& rs, float& r2, float& cr, int& idx, float& rf) const {
     return list_rec(ovRec, k, rs, r2, cr, idx, rf);
@@ -872,8 +876,8 @@ extern "C" void hostsim_list_records(const rtg_sphere* spheres, unsigned n,
   out[2] = ps.bvhNodes.size() / (rtg::kBvhWords * rtg::kBvhCopies);
   rtg::sphere_lists(spheres, n, lights, m, &ps, (size_t)maxRecords);
   if (ps.capOff.empty()) return;
-  out[0] = ps.capRec.size() / rtg::kListWords - 1;  // without the padding record
-  out[1] = ps.ovRec.size() / rtg::kListWords - 1;
+  out[0] = ps.capRec.size() / rtg::kCapWords - rtg::kCapPad;  // without the padding records
+  out[1] = ps.ovRec.size() / rtg::kListWords - rtg::kOvPad;
 }
 
 // `behind` (rtg_trace.h) never rejects a sphere the reference's root test
@@ -985,5 +989,35 @@ extern "C" long hostsim_no_root_check(long trials, unsigned long long seed, long
       if (res) ++bad;
     }
   }
+  return bad;
+}
+
+// cap_screen_r2 (rtg_trace.h, the device's screen radius^2 of a 16-byte
+// capsule record) never falls below the host's screen_r2, which pass1_rad's
+// conservativeness argument assumes: every non-negative binary32 value r2 at
+// a stride (all subnormals and the values around every power of two below
+// it included), plus inf and NaN.  Returns the violations; *checked counts
+// the values tested.
+extern "C" long hostsim_cap_screen_check(unsigned stride, long* checked) {
+  long bad = 0;
+  *checked = 0;
+  auto one = [&](uint32_t bits) {
+    float r2;
+    memcpy(&r2, &bits, 4);
+    const float a = rtg::cap_screen_r2(r2), b = rtg::screen_r2(r2);
+    ++*checked;
+    if (r2 != r2) {
+      if (a == a) ++bad;
+    } else if (!(a >= b)) {
+      ++bad;
+    }
+  };
+  for (uint64_t u = 0; u <= 0x7FC00000u; u += stride) one((uint32_t)u);
+  for (uint32_t e = 0; e < 256; ++e)  // both sides of every binade boundary
+    for (uint32_t m = 0; m < 64; ++m) {
+      one((e << 23) + m);
+      if (e > 0) one((e << 23) - 1 - m);
+    }
+  for (uint32_t m = 0; m < 0x800000u; m += 7) one(m);  // subnormals
   return bad;
 }

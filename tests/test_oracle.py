@@ -433,8 +433,11 @@ def test_sphere_list_limits(hostsim, golden, rtg):
     f(P(sph), len(sph), P(lg), len(lg), 1 << 23, out)
     cap, ov, nodes = list(out)
     assert cap > 0 and ov > 0 and nodes > 0, list(out)
-    assert (cap + 1) * 32 < 2 ** 32 and (ov + 1) * 32 < 2 ** 32
-    budget = max(cap, ov)  # the larger table just over the budget: no lists
+    # padding records: capsule tables 3 (16-byte records, four per scalar
+    # load), overlap tables 1 (32-byte records, two per load)
+    cpad, opad = 3, 1
+    assert (cap + cpad) * 16 < 2 ** 32 and (ov + opad) * 32 < 2 ** 32
+    budget = max(cap + cpad, ov + opad) - 1  # the larger table just over the budget: no lists
     f(P(sph), len(sph), P(lg), len(lg), budget, out)
     assert out[0] == 0 and out[1] == 0 and out[2] == nodes
     f(P(sph), len(sph), P(lg), len(lg), budget + 1, out)
@@ -489,6 +492,20 @@ def test_behind_is_exact(hostsim):
     assert bad == 0, bad
     assert rej.value > 1_000_000, rej.value
     assert loose.value > 0, loose.value
+
+
+def test_cap_screen_r2_is_conservative(hostsim):
+    """The device's screen radius^2 of a 16-byte capsule record
+    (cap_screen_r2: fma(r2, C, 2^-149), rtg_trace.h) is never below the host's
+    screen_r2, the bound pass1_rad's screen is proven with: every 61st
+    non-negative binary32 value, both sides of every binade boundary, every
+    7th subnormal, inf and NaN (NaN stays NaN)."""
+    f = hostsim.hostsim_cap_screen_check
+    f.restype = ctypes.c_long
+    checked = ctypes.c_long(0)
+    bad = f(ctypes.c_uint(61), ctypes.byref(checked))
+    assert bad == 0, bad
+    assert checked.value > 30_000_000, checked.value
 
 
 def test_no_root_is_exact(hostsim):
