@@ -286,7 +286,7 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
 constexpr int kListWords = 8;
 // records read past a list's end by one load: padding at each table's end
 constexpr int kCapPad = 64 / (4 * kCapWords) - 1;
-constexpr int kOvPad = RTG_OV4 ? 3 : 1;
+constexpr int kOvPad = 1;
 constexpr size_t kListMaxRecords = size_t(1) << 23;
 constexpr double kListMaxTests = 0x1p28;
 inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light* lights,
@@ -350,7 +350,7 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
     for (unsigned j = 0; j < n; ++j)
       if (overlap_keep(spheres, h, j)) ov[h].push_back(j);
     ovTotal += ov[h].size();
-    if (ovTotal + kOvPad > maxRecords) return;
+    if (ovTotal + 1 > maxRecords) return;
   }
   ps->capRec.reserve((capTotal + kCapPad) * kCapWords);
   ps->capOff.push_back(0);
@@ -366,32 +366,11 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
     }
     ps->capOff.push_back((unsigned)(ps->capRec.size() / kCapWords));
   }
+  ps->ovRec.reserve((ovTotal + 1) * kListWords);
   ps->ovOff.push_back(0);
-  if (RTG_OV4) {
-    // three tables of `stride` records: {c, r^2}, {c, (r + 1e-6f)^2}, indices
-    const size_t stride = ovTotal + kOvPad;
-    ps->ovRec.assign(stride * 9, NAN);
-    size_t k = 0;
-    for (unsigned h = 0; h < n; ++h) {
-      for (unsigned j : ov[h]) {
-        const rtg_sphere& sp = spheres[j];
-        const float rc = sp.radius + 1.0e-6f;  // raytracer.h:259-264
-        const float e[4] = {sp.pos.x, sp.pos.y, sp.pos.z, sp.radius * sp.radius};
-        const float c[4] = {sp.pos.x, sp.pos.y, sp.pos.z, rc * rc};
-        memcpy(&ps->ovRec[4 * k], e, sizeof e);
-        memcpy(&ps->ovRec[4 * (stride + k)], c, sizeof c);
-        memcpy(&ps->ovRec[8 * stride + k], &j, 4);
-        ++k;
-      }
-      ps->ovOff.push_back((unsigned)k);
-    }
-    ps->ovOff.push_back((unsigned)stride);  // ovOff[n + 1]: the table stride
-  } else {
-    ps->ovRec.reserve((ovTotal + kOvPad) * kListWords);
-    for (unsigned h = 0; h < n; ++h) {
-      for (unsigned j : ov[h]) rec(ps->ovRec, j);
-      ps->ovOff.push_back((unsigned)(ps->ovRec.size() / kListWords));
-    }
+  for (unsigned h = 0; h < n; ++h) {
+    for (unsigned j : ov[h]) rec(ps->ovRec, j);
+    ps->ovOff.push_back((unsigned)(ps->ovRec.size() / kListWords));
   }
   // padding records past each table's end: the kernel reads a 64-byte
   // scalar load of records at a time (two overlap records, four capsule
@@ -399,8 +378,7 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
   // whose NaN centres accept no root
   const float pad[kListWords] = {NAN, NAN, NAN, NAN, NAN, NAN, 0.f, 1.f};
   for (int k = 0; k < kCapPad; ++k) ps->capRec.insert(ps->capRec.end(), pad, pad + kCapWords);
-  if (!RTG_OV4)  // (the 16-byte tables were NaN-filled, padding included)
-    for (int k = 0; k < kOvPad; ++k) ps->ovRec.insert(ps->ovRec.end(), pad, pad + kListWords);
+  for (int k = 0; k < kOvPad; ++k) ps->ovRec.insert(ps->ovRec.end(), pad, pad + kListWords);
 }
 
 inline float round_up_f(double v) {

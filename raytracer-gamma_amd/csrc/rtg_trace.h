@@ -1372,15 +1372,6 @@ struct ListRec {
 #define RTG_CAP_WORDS 4
 #endif
 constexpr int kCapWords = RTG_CAP_WORDS;
-// Overlap-list records: RTG_OV4 = 1 (the default) three tables of one stride
-// each, {x, y, z, r^2} (entering rays), {x, y, z, (r + 1e-6f)^2}
-// (containment) and the sphere indices, the records four to a 64-byte scalar
-// load and the index read once per query for the winning position; 0 (A/B
-// builds) the 32-byte records {x, y, z, screen r^2, r^2, (r + 1e-6f)^2,
-// index, refractive index}, two to a load.
-#ifndef RTG_OV4
-#define RTG_OV4 1
-#endif
 // One capsule-list record (16-byte form, kCapWords == 4): centre and r^2.
 struct CapRec {
   V3 c;
@@ -1688,36 +1679,9 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
   tOut = 1000.f;
   if (!sc.all(ok)) return -1;
   float minT = th;
+  int best = h;
   unsigned k0, k1;
   sc.ov_range((unsigned)h, k0, k1);
-#if RTG_OV4
-  // Four 16-byte {c, r^2} records per scalar load, h's own included (its
-  // exact test gives th again: the same operations on the same values), the
-  // winner kept as a list POSITION: the list is in index order, so positions
-  // order its spheres as their indices do, and the records past its end (the
-  // next list's, or the padding) can have no accepted root at t <= th (the
-  // overlap lists' argument: no sphere outside h's list has one before the
-  // exit point), so they never tie or win.  The winner's index is then one
-  // per-lane read of the index table.
-  int bestPos = 0x7FFFFFFF;
-  for (unsigned k = k0; k < k1; k += 4) {  // wave-uniform
-    CapRec r[4];
-    sc.ov_rec4(k, 0, r);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sc.count(kUOvIter, 1);
-      if (screen_ahead(q, r[j].c, cap_screen_r2(r[j].r2))) {
-        sc.count(kUEnterExact, 1);
-        bool rj;
-        const float t = ray_sphere_leaf(q, r[j].c, r[j].r2, rj);
-        take_closer(t, (int)(k + j), minT, bestPos);
-      }
-    }
-  }
-  tOut = minT;
-  return sc.ov_index((unsigned)bestPos);
-#else
-  int best = h;
   auto step = [&](const ListRec& r) {
     const int j = r.idx;
     if (j == h) return;
@@ -1740,7 +1704,6 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
   }
   tOut = minT;
   return best;
-#endif
 }
 
 // primary_container (raytracer.h:245-270) for refraction test points of hits
@@ -1749,31 +1712,10 @@ RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut
 // argument of primary_container_sel), and its refractive index in nT.
 template <class Scene>
 RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
-  unsigned k0, k1;
-  sc.ov_range((unsigned)h, k0, k1);
-#if RTG_OV4
-  // Four 16-byte {c, (r + 1e-6f)^2} records per scalar load; the first
-  // containing POSITION (the list is in index order), then its index and
-  // refractive index per lane.  A sphere past the list's end cannot contain
-  // the point (every container is listed).
-  int pos = -1;
-  for (unsigned k = k0; k < k1; k += 4) {  // wave-uniform
-    CapRec r[4];
-    sc.ov_rec4(k, 1, r);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sc.count(kUOvIter, 1);
-      const V3 dist = vsub(pt, r[j].c);
-      if (pos < 0 && vdot(dist, dist) <= r[j].r2) pos = (int)(k + j);
-    }
-    if (sc.all(pos >= 0)) break;
-  }
-  const int found = pos < 0 ? -1 : sc.ov_index((unsigned)pos);
-  nT = sc.refr(found < 0 ? (int)sc.n : found);
-  return found;
-#else
   int found = -1;
   nT = sc.refr((int)sc.n);  // background material
+  unsigned k0, k1;
+  sc.ov_range((unsigned)h, k0, k1);
   auto step = [&](const ListRec& r) {
     sc.count(kUOvIter, 1);
     const V3 dist = vsub(pt, r.c);
@@ -1792,7 +1734,6 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
     if (sc.all(found >= 0)) break;
   }
   return found;
-#endif
 }
 
 // The list queries above for waves whose lanes hit different spheres (every

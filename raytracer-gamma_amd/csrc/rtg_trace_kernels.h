@@ -297,24 +297,6 @@ struct DevScene {
       r[j].r2 = g[4 * j + 3];
     }
   }
-  // Overlap records k .. k + 3 of table `tab` (0: {c, r^2}, 1: {c, (r +
-  // 1e-6f)^2}; 16-byte form, RTG_OV4) with one 64-byte scalar load; the
-  // tables are ovOff[n + 1] records apart, then the sphere indices.
-  __device__ __forceinline__ void ov_rec4(unsigned k, unsigned tab, CapRec* r) const {
-    typedef float f16 __attribute__((ext_vector_type(16)));
-    const unsigned base = tab ? 4u * uidx(ovOff, n + 1)[0] : 0u;
-    const f16 g = *(const RTG_CONST f16*)fidx(ovRec, base + 4u * k);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      r[j].c = v3(g[4 * j], g[4 * j + 1], g[4 * j + 2]);
-      r[j].r2 = g[4 * j + 3];
-    }
-  }
-  // The sphere index at list position pos (per lane).
-  __device__ __forceinline__ int ov_index(unsigned pos) const {
-    const unsigned stride = uidx(ovOff, n + 1)[0];
-    return __float_as_int(*fidx(ovRec, 8u * stride + pos));
-  }
   __device__ __forceinline__ void ov_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
   }

@@ -68,19 +68,6 @@ struct HostScene {
       r[j].r2 = g[3];
     }
   }
-  void ov_rec4(unsigned k, unsigned tab, rtg::CapRec* r) const {
-    const size_t base = tab ? 4 * (size_t)ovOff[n + 1] : 0;
-    for (int j = 0; j < 4; ++j) {
-      const float* g = ovRec + base + 4 * ((size_t)k + j);
-      r[j].c = rtg::v3(g[0], g[1], g[2]);
-      r[j].r2 = g[3];
-    }
-  }
-  int ov_index(unsigned pos) const {
-    int i;
-    memcpy(&i, ovRec + 8 * (size_t)ovOff[n + 1] + pos, 4);
-    return i;
-  }
   void ov_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
     list_rec2(ovRec, k, r0, r1);
   }
@@ -890,7 +877,7 @@ extern "C" void hostsim_list_records(const rtg_sphere* spheres, unsigned n,
   rtg::sphere_lists(spheres, n, lights, m, &ps, (size_t)maxRecords);
   if (ps.capOff.empty()) return;
   out[0] = ps.capRec.size() / rtg::kCapWords - rtg::kCapPad;  // without the padding records
-  out[1] = RTG_OV4 ? ps.ovOff[n + 1] - rtg::kOvPad : ps.ovRec.size() / rtg::kListWords - rtg::kOvPad;
+  out[1] = ps.ovRec.size() / rtg::kListWords - rtg::kOvPad;
 }
 
 // `behind` (rtg_trace.h) never rejects a sphere the reference's root test

@@ -433,10 +433,10 @@ def test_sphere_list_limits(hostsim, golden, rtg):
     f(P(sph), len(sph), P(lg), len(lg), 1 << 23, out)
     cap, ov, nodes = list(out)
     assert cap > 0 and ov > 0 and nodes > 0, list(out)
-    # padding records: 3 per table (16-byte records, four per scalar load;
-    # the overlap lists' three tables, 36 bytes per record in all)
-    cpad, opad = 3, 3
-    assert (cap + cpad) * 16 < 2 ** 32 and (ov + opad) * 36 < 2 ** 32
+    # padding records: capsule tables 3 (16-byte records, four per scalar
+    # load), overlap tables 1 (32-byte records, two per load)
+    cpad, opad = 3, 1
+    assert (cap + cpad) * 16 < 2 ** 32 and (ov + opad) * 32 < 2 ** 32
     budget = max(cap + cpad, ov + opad) - 1  # the larger table just over the budget: no lists
     f(P(sph), len(sph), P(lg), len(lg), budget, out)
     assert out[0] == 0 and out[1] == 0 and out[2] == nodes
