@@ -682,6 +682,12 @@ def main():
                 if vi and work is not None:
                     roof["pmc_valu_insts"] = int(vi)
                     roof["model_vs_pmc_valu"] = round(work["valu_slots"] / vi, 3)
+                    # the unit prices are FITTED to SQ_INSTS_VALU over a scene
+                    # set that includes the bench configs (tools/calib_units.py),
+                    # so this ratio is in-sample; the held-out figures are in
+                    # the fit record
+                    roof["model_vs_pmc_valu_kind"] = (
+                        "fitted (in sample); held-out ratios: rtg_amd/work.py FIT_RECORD")
                 if vi:
                     # the same roofline from the hardware's count of executed
                     # VALU wave instructions (x 64 lanes) per launch, over this

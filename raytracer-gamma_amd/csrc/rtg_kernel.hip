@@ -836,12 +836,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   }
   const bool sampleKernel = vi->kind == kVariantSample;
   // the default sample kernel reads materials/geometry from global memory
-  // (L1/L2-resident), not from a per-workgroup LDS copy (variant 17 keeps it)
-  // (as do the shipped tile kernels 9, 59, 100); only the A/B variants below
-  // stage it
+  // (L1/L2-resident), not from a per-workgroup LDS copy (as do the shipped
+  // tile kernels 9, 59, 100); only the A/B variants below stage it
   if (!(variant == 1 || variant == 2 || variant == 3 || variant == 4 || variant == 5 ||
-        variant == 6 || variant == 8 || variant == 14 || variant == 16 || variant == 17 ||
-        variant == 104 || variant == 108))
+        variant == 6 || variant == 8 || variant == 14 || variant == 104 || variant == 108))
     ldsMats = false;
   unsigned rows;
   if (rowList) {
@@ -925,7 +923,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     const size_t groupsPerWave = variant == 21 ? 4 : 1;
     const size_t groups = ((size_t)width * rows + ppw - 1) / ppw;
     const size_t waves = (groups + groupsPerWave - 1) / groupsPerWave;
-    const unsigned tpb = variant == 14 ? 256u : variant == 16 ? 128u : 64u;
+    const unsigned tpb = variant == 14 ? 256u : 64u;
     const size_t blocks = (waves + tpb / 64 - 1) / (tpb / 64);
     threads = tpb;
     if (blocks > 0x7FFFFFFFu) {

@@ -262,6 +262,125 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
   }
 }
 
+// Hit-point cells of the capsule lists (BVH scenes).  A shadow ray starts at
+// a hit point P of sphere h; the kernel classifies e = P - c_h (cap_cell,
+// rtg_trace.h) into one of 24 cells: the axis a of e's largest component
+// and the signs of e's three components, and only when |e| >= r_in =
+// |r_h| (1 - 2^-8) (cells need the shell; else, or when the guard test
+// fails, kCapFull).  Every classified P then lies in the cell's region
+//   R = { c_h + e : r_in <= |e| <= g_h, e_a has the cell's sign, |e_a| >=
+//         (1 - 2^-20) max(|e_p|, |e_q|), e_p, e_q have the cell's signs }
+// (the computed e's signs are exact: one rounded subtraction each; its
+// largest component can be 2^-23 below another's; its |e|^2 test is argued at
+// cap_cell).  In gnomonic coordinates on face a the directions of R fill the
+// rectangle [0, 1 + 2^-19]^2 (signed), so every direction of R is within the
+// angle theta of the rectangle's centre direction v0 that its farthest corner
+// has (the cap around v0 is convex in those coordinates), and R lies in the
+// ball around c_h + beta v0 whose radius reaches the points at angle theta
+// at |e| = r_in and |e| = g_h (cell_ball).  The segment P -> L lies within
+// that radius of the segment b -> L, so the capsule argument of
+// shadow_masks holds with (b, rho) in place of (c_h, g_h): a cell keeps the
+// spheres of the full capsule list whose grown ball meets that capsule
+// (cell_keep).  C5: 45 -> 25 capsule records per list on average.
+inline double g_cellBallSlack = 0.0;  // test hook (tests/hostsim): shrinks the cell balls
+inline double cell_rin(const rtg_sphere& s) {
+  const double r = fabs((double)s.radius);
+  return r < 0x1p-60 ? 0.0 : r * (1.0 - 0x1p-8);
+}
+// Centre b and radius rho of the ball holding cell `cell`'s region of sphere s.
+inline void cell_ball(const rtg_sphere& s, unsigned cell, double b[3], double* rho) {
+  const unsigned a = cell >> 3, p = a == 0 ? 1 : 0, q = a == 2 ? 1 : 2;
+  const double sa = (cell & 4) ? -1.0 : 1.0, sp = (cell & 2) ? -1.0 : 1.0,
+               sq = (cell & 1) ? -1.0 : 1.0;
+  const double E = 1.0 + 0x1p-19;
+  auto dir = [&](double pp, double qq, double v[3]) {
+    v[a] = sa;
+    v[p] = sp * pp;
+    v[q] = sq * qq;
+    const double l = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    for (int k = 0; k < 3; ++k) v[k] /= l;
+  };
+  double v0[3];
+  dir(0.5 * E, 0.5 * E, v0);
+  double cmin = 1.0;
+  for (int k = 0; k < 4; ++k) {
+    double v[3];
+    dir((k & 1) ? E : 0.0, (k & 2) ? E : 0.0, v);
+    const double c = v[0] * v0[0] + v[1] * v0[1] + v[2] * v0[2];
+    cmin = c < cmin ? c : cmin;
+  }
+  cmin -= 1e-12;  // theta rounded up
+  const double ri = cell_rin(s), g = guard_radius(s);
+  auto f = [&](double beta) {  // squared distance to the farthest extreme point
+    const double f1 = ri * ri + beta * beta - 2.0 * ri * beta * cmin;
+    const double f2 = g * g + beta * beta - 2.0 * g * beta * cmin;
+    return f1 > f2 ? f1 : f2;
+  };
+  // the minimum of the larger of two convex parabolas: at one's vertex or
+  // where they cross
+  double best = 1e300, bb = 0.0;
+  const double cand[3] = {ri * cmin, g * cmin, cmin > 0.0 ? (g + ri) / (2.0 * cmin) : 0.0};
+  for (double beta : cand) {
+    beta = beta < 0.0 ? 0.0 : beta;
+    if (f(beta) < best) { best = f(beta); bb = beta; }
+  }
+  b[0] = s.pos.x + bb * v0[0];
+  b[1] = s.pos.y + bb * v0[1];
+  b[2] = s.pos.z + bb * v0[2];
+  const double cm = fabs((double)s.pos.x) + fabs((double)s.pos.y) + fabs((double)s.pos.z);
+  *rho = sqrt(best) * (1.0 + 1e-9) * (1.0 - g_cellBallSlack) + 1e-12 * (g + cm);
+}
+// Is cell `cell` of sphere h wholly behind the plane through c_h facing
+// light L (every direction e with e.u < 0)?  Such a cell holds no point a
+// shadow ray is cast from (capsule_keep's back plane), so it shares the
+// full list instead of a list of its own.
+inline bool cell_behind(const rtg_sphere& s, unsigned cell, const double L[3]) {
+  const unsigned a = cell >> 3, p = a == 0 ? 1 : 0, q = a == 2 ? 1 : 2;
+  const double sa = (cell & 4) ? -1.0 : 1.0, sp = (cell & 2) ? -1.0 : 1.0,
+               sq = (cell & 1) ? -1.0 : 1.0;
+  const double u[3] = {L[0] - s.pos.x, L[1] - s.pos.y, L[2] - s.pos.z};
+  const double ul = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+  if (!(ul > 2.0 * guard_radius(s))) return false;  // (the back plane's condition)
+  const double E = 1.0 + 0x1p-19;
+  for (int k = 0; k < 4; ++k) {  // e.u is linear in the gnomonic coordinates
+    const double pp = (k & 1) ? E : 0.0, qq = (k & 2) ? E : 0.0;
+    if (sa * u[a] + sp * pp * u[p] + sq * qq * u[q] > -1e-3 * ul) return false;
+  }
+  return true;
+}
+// Sphere i in cell `cell`'s capsule list for light L: its grown ball meets the
+// capsule of radius rho around b -> L (cell_ball), with capsule_keep's margin.
+inline bool cell_keep(const rtg_sphere* spheres, unsigned h, unsigned i, const double L[3],
+                      const double b[3], double rho) {
+  if (i == h) return true;
+  const rtg_sphere& sh = spheres[h];
+  const rtg_sphere& si = spheres[i];
+  const double g = guard_radius(sh);
+  const double C[3] = {si.pos.x, si.pos.y, si.pos.z};
+  const double ri = fabs((double)si.radius);
+  double ab[3], ab2 = 0.0, t = 0.0, dch = 0.0, lh = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    ab[k] = L[k] - b[k];
+    ab2 += ab[k] * ab[k];
+    t += (C[k] - b[k]) * ab[k];
+    const double ch = C[k] - (k == 0 ? sh.pos.x : k == 1 ? sh.pos.y : sh.pos.z);
+    dch += ch * ch;
+    const double lc = L[k] - (k == 0 ? sh.pos.x : k == 1 ? sh.pos.y : sh.pos.z);
+    lh += lc * lc;
+  }
+  dch = sqrt(dch);
+  lh = sqrt(lh);
+  t = ab2 > 0.0 ? t / ab2 : 0.0;
+  t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+  double d2 = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double e = C[k] - (b[k] + t * ab[k]);
+    d2 += e * e;
+  }
+  const double mu = 0x1p-8 * (dch + g + ri) + 0x1p-16 * (lh + g);
+  return !(sqrt(d2) > (rho + ri + mu) * (1.0 + 1e-9));
+}
+
 // Sphere lists of BVH scenes (n > 64, where 64-bit masks do not reach): the
 // masks' sets as lists of kListWords-word records, for the coherent-wave
 // queries of rtg_trace.h (blocked_cap, closest_enter_list, container_list):
@@ -273,8 +392,11 @@ inline void shadow_masks(const rtg_sphere* spheres, unsigned n, const rtg_light*
 //  * overlap lists, one per sphere h: the spheres of overlap mask h
 //    (overlap_keep) in index order, records {x, y, z, screen r^2, r^2,
 //    (r + 1e-6f)^2, index, refractive index}.
-// capOff[l n + h] .. capOff[l n + h + 1] and ovOff[h] .. ovOff[h + 1] index
-// the records.  Empty for non-finite scenes (the queries then use the BVH).
+// capOff[2 ((l n + h) kCapCells + c)] and [... + 1] delimit the capsule list of
+// (light l, sphere h, hit-point cell c) (cells above; kCapFull the whole
+// capsule list, which cells wholly behind the light's plane share), and
+// ovOff[h] .. ovOff[h + 1] the overlap list.  Empty for non-finite scenes
+// (the queries then use the BVH).
 //
 // Limits.  The kernel addresses the record tables with 32-bit byte offsets
 // (fidx(capRec, 8k): 32 k bytes), and the lists grow as O(m n^2) records, so
@@ -295,7 +417,7 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
   ps->capOff.clear();
   ps->ovRec.clear();
   ps->ovOff.clear();
-  if ((double)(m + 1) * n * n > kListMaxTests) return;
+  if ((double)(m + 1) * n * n > kListMaxTests) return;  // (cells test only full-list members)
   auto finite = [](double v) { return v == v && fabs(v) <= 1e30; };
   for (unsigned i = 0; i < n; ++i)
     if (!finite(spheres[i].pos.x) || !finite(spheres[i].pos.y) || !finite(spheres[i].pos.z) ||
@@ -315,9 +437,13 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
                                  s.material.refractiveIndex};
     v.insert(v.end(), w, w + kListWords);
   };
-  // capsule lists: per (l, h) the kept spheres sorted by capsule_keep's key;
-  // the (l, h) pairs are independent, so they are built in parallel
+  // capsule lists: per (l, h) the kept spheres sorted by capsule_keep's key,
+  // then per cell the members its capsule keeps, in the same order (cells
+  // wholly behind the light's plane: none, they share the full list); the
+  // (l, h) pairs are independent, so they are built in parallel
   std::vector<std::vector<unsigned>> lists((size_t)m * n);
+  std::vector<std::vector<unsigned>> cells((size_t)m * n * kCapCubeCells);
+  std::vector<unsigned char> cellShared((size_t)m * n * kCapCubeCells, 0);
   auto work = [&](unsigned lo, unsigned hi) {
     std::vector<std::pair<double, unsigned>> tmp;
     for (unsigned q = lo; q < hi; ++q) {
@@ -330,6 +456,17 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
       }
       std::sort(tmp.begin(), tmp.end());
       for (const auto& e : tmp) lists[q].push_back(e.second);
+      for (unsigned c = 0; c < kCapCubeCells; ++c) {
+        const size_t qc = (size_t)q * kCapCubeCells + c;
+        if (cell_behind(spheres[h], c, L)) {
+          cellShared[qc] = 1;
+          continue;
+        }
+        double b[3], rho;
+        cell_ball(spheres[h], c, b, &rho);
+        for (unsigned i : lists[q])
+          if (cell_keep(spheres, h, i, L, b, rho)) cells[qc].push_back(i);
+      }
     }
   };
   const unsigned total = m * n;
@@ -343,6 +480,7 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
   for (auto& th : pool) th.join();
   size_t capTotal = 0;
   for (const auto& l : lists) capTotal += l.size();
+  for (const auto& l : cells) capTotal += l.size();
   if (capTotal + kCapPad > maxRecords) return;  // (the padding records)
   std::vector<std::vector<unsigned>> ov(n);
   size_t ovTotal = 0;
@@ -353,18 +491,28 @@ inline void sphere_lists(const rtg_sphere* spheres, unsigned n, const rtg_light*
     if (ovTotal + 1 > maxRecords) return;
   }
   ps->capRec.reserve((capTotal + kCapPad) * kCapWords);
-  ps->capOff.push_back(0);
+  ps->capOff.assign((size_t)total * kCapCells * 2, 0u);
+  auto emit = [&](const std::vector<unsigned>& li, size_t slot) {
+    ps->capOff[2 * slot] = (unsigned)(ps->capRec.size() / kCapWords);
+    for (unsigned i : li) {
+      const rtg_sphere& sp = spheres[i];
+      const float w[kCapWords] = {sp.pos.x, sp.pos.y, sp.pos.z, sp.radius * sp.radius};  // raytracer.h:100
+      ps->capRec.insert(ps->capRec.end(), w, w + kCapWords);
+    }
+    ps->capOff[2 * slot + 1] = (unsigned)(ps->capRec.size() / kCapWords);
+  };
   for (unsigned q = 0; q < total; ++q) {
-    for (unsigned i : lists[q]) {
-      if (kCapWords == kListWords) {
-        rec(ps->capRec, i);
+    const size_t full = (size_t)q * kCapCells + kCapFull;
+    emit(lists[q], full);
+    for (unsigned c = 0; c < kCapCubeCells; ++c) {
+      const size_t qc = (size_t)q * kCapCubeCells + c, slot = (size_t)q * kCapCells + c;
+      if (cellShared[qc]) {
+        ps->capOff[2 * slot] = ps->capOff[2 * full];
+        ps->capOff[2 * slot + 1] = ps->capOff[2 * full + 1];
       } else {
-        const rtg_sphere& sp = spheres[i];
-        const float w[4] = {sp.pos.x, sp.pos.y, sp.pos.z, sp.radius * sp.radius};  // raytracer.h:100
-        ps->capRec.insert(ps->capRec.end(), w, w + 4);
+        emit(cells[qc], slot);
       }
     }
-    ps->capOff.push_back((unsigned)(ps->capRec.size() / kCapWords));
   }
   ps->ovRec.reserve((ovTotal + 1) * kListWords);
   ps->ovOff.push_back(0);

@@ -546,6 +546,33 @@ constexpr double kConeHalf[kConeTiers] = {0.20943951023931953,   // 12 degrees
 constexpr float kConeCos[kConeTiers] = {0.97814760073380569f,   // cos, rounded up
                                         0.81915204428899179f};
 
+// Hit-point cells of the capsule lists (BVH scenes; the geometry and why
+// each cell's list holds every possible blocker: rtg_scene_pack.h, above
+// cell_ball): 24 cells by e = P - c_h's largest axis and its components'
+// signs, and kCapFull (the whole capsule list) for points the cells do not
+// cover.
+constexpr unsigned kCapCubeCells = 24;
+constexpr unsigned kCapCells = kCapCubeCells + 1;
+constexpr unsigned kCapFull = kCapCubeCells;
+// The cell of hit point P = c_h + e on a sphere of r^2 = r2 (the float r * r
+// of raytracer.h:100).  Needs |e| >= r_in = |r| (1 - 2^-8): |e|^2 computed
+// (relative error < 5 2^-24) >= r2 (1 - 2^-9) computed implies it for
+// r2 >= 2^-120 (cell_rin takes r_in = 0 below |r| = 2^-60), else kCapFull.
+// The signs of the computed components are exact (one rounded subtraction
+// each) and the largest computed component is within 2^-23 of the exact
+// largest, which the cells' regions allow for.  NaN: kCapFull.
+RTG_HD unsigned cap_cell(V3 e, float r2) {
+  const float d2 = vdot(e, e);
+  if (!(d2 >= r2 * 0x1.ffp-1f)) return kCapFull;
+  const float ax = fabsf(e.x), ay = fabsf(e.y), az = fabsf(e.z);
+  const bool xm = ax >= ay && ax >= az, ym = !xm && ay >= az;
+  const float va = xm ? e.x : ym ? e.y : e.z;
+  const float vp = xm ? e.y : e.x;
+  const float vq = ym || xm ? e.z : e.y;
+  return (xm ? 0u : ym ? 8u : 16u) + (va < 0.f ? 4u : 0u) + (vp < 0.f ? 2u : 0u) +
+         (vq < 0.f ? 1u : 0u);
+}
+
 // Cube-map cell of direction U (any length): the face of the major axis and
 // a kConeGrid x kConeGrid grid over the other two coordinates / |major|.  A
 // direction near a cell border may land in either cell; the masks' 1e-3 rad
@@ -583,11 +610,13 @@ RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap);
 template <class Scene>
 RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel);
 template <class Scene>
-RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h);
+RTG_HD bool blocked_cap(const Scene& sc, const RayQ& q, float gap, unsigned l, int h,
+                        unsigned cell);
 template <class Scene>
 RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
-RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h);
+RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h,
+                              unsigned cell, V3 ch, float r2h);
 template <class Scene>
 RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut);
 // Most distinct spheres a wave walks the per-sphere lists of (blocked_cap_lanes
@@ -596,6 +625,11 @@ RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut);
 #define RTG_LIST_WALKS 5
 #endif
 constexpr int kListWalks = RTG_LIST_WALKS;
+// ... and for shadow rays, whose walks are keyed by (sphere, hit-point cell)
+#ifndef RTG_SHADOW_WALKS
+#define RTG_SHADOW_WALKS 8
+#endif
+constexpr int kShadowWalks = RTG_SHADOW_WALKS;
 template <class Scene>
 RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
@@ -613,7 +647,8 @@ struct IsBvhScene<S, std::void_t<decltype(S::kIsBvh)>> : std::bool_constant<S::k
 // (shadow_masks, rtg_scene_pack.h) for the hit sphere `hit`; `guardOK` tells
 // that P lies in that sphere's guard ball (else every sphere is tested).
 template <int Q, class Scene>
-RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = false) {
+RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = false,
+                      unsigned cell = kCapFull, V3 hc = V3{}, float hr2 = 0.f) {
   V3 sum = v3(0.f, 0.f, 0.f);
   const unsigned m = sc.m;
   for (unsigned l = 0; l < m; ++l) {
@@ -655,7 +690,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
           // BVH scene: each lane's hit sphere's capsule list for light l, the
           // wave's distinct hit spheres in turn (blocked_cap_lanes)
           if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagShdSame, 1);
-          blk = blocked_cap_lanes(sc, P, dir, gap, l, hit);
+          blk = blocked_cap_lanes(sc, P, dir, gap, l, hit, cell, hc, hr2);
         } else {
           blk = query_blocked<2>(sc, P, dir, gap);
         }
@@ -843,6 +878,47 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
   return tgt;
 }
 
+// The reflection-child records in private memory (trace_sample's fr[]):
+// BVH scenes (C5: S = 8, 54 GB of record traffic per frame) store and load
+// them with the nontemporal (streaming) policy, so they do not push the scene's
+// node and list lines out of the caches: C5 -1 to -1.2 %;
+// the masked scenes keep the default policy (C3 +7.5 %, C4 +6.6 % with it:
+// their records are re-read while still cached).
+template <bool kNT>
+RTG_HD void store_frame_r(FrameR& dst, const FrameR& r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kNT) {
+    __builtin_nontemporal_store(r.ro.x, &dst.ro.x);
+    __builtin_nontemporal_store(r.ro.y, &dst.ro.y);
+    __builtin_nontemporal_store(r.ro.z, &dst.ro.z);
+    __builtin_nontemporal_store(r.rd.x, &dst.rd.x);
+    __builtin_nontemporal_store(r.rd.y, &dst.rd.y);
+    __builtin_nontemporal_store(r.rd.z, &dst.rd.z);
+    __builtin_nontemporal_store(r.rI.x, &dst.rI.x);
+    __builtin_nontemporal_store(r.rI.y, &dst.rI.y);
+    __builtin_nontemporal_store(r.rI.z, &dst.rI.z);
+    return;
+  }
+#endif
+  dst = r;
+}
+template <bool kNT>
+RTG_HD FrameR load_frame_r(const FrameR& src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (kNT) {
+    FrameR r;
+    r.ro = v3(__builtin_nontemporal_load(&src.ro.x), __builtin_nontemporal_load(&src.ro.y),
+              __builtin_nontemporal_load(&src.ro.z));
+    r.rd = v3(__builtin_nontemporal_load(&src.rd.x), __builtin_nontemporal_load(&src.rd.y),
+              __builtin_nontemporal_load(&src.rd.z));
+    r.rI = v3(__builtin_nontemporal_load(&src.rI.x), __builtin_nontemporal_load(&src.rI.y),
+              __builtin_nontemporal_load(&src.rI.z));
+    return r;
+  }
+#endif
+  return src;
+}
+
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
 // kCL: the reference OpenCL kernel's semantics (raytrace_kernel.cl:641-867):
@@ -947,25 +1023,27 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       sc.count(kUShade, 1);
       sc.probe_begin(kProbeSplitSetup);
       V3 c;
-      float g2;
+      float g2, r2h;
       Mat mh;
-      sc.hit_data(hit, c, g2, mh);  // centre, guard radius^2, material of the hit sphere
+      sc.hit_data(hit, c, g2, r2h, mh);  // centre, guard radius^2, r^2, material of the hit sphere
       const V3 P = vadd(o, vsmul(t, d));
       const V3 N = vnorm(vsub(P, c));
       const float op = mh.opacity;
       const float tr = 1.f - op;
       V3 colour = v3(0.f, 0.f, 0.f);
       bool guardOK = false;
+      unsigned cell = kCapFull;  // the hit point's capsule-list cell (BVH scenes)
       if constexpr (Q == 4) {  // P in the hit sphere's guard ball (shadow/overlap masks)
         const V3 e = vsub(P, c);
         guardOK = vdot(e, e) <= g2;
+        if (sc.has_lists() && guardOK) cell = cap_cell(e, r2h);
       }
       sc.probe_end(kProbeSplitSetup);
       if (op > 0.f) {
         V3 tmp = vmul(I, mh.matte);
         tmp = vsmul(op, tmp);
         sc.probe_begin(kProbeMatte);
-        const V3 mc = matte_light<Q>(sc, P, N, hit, guardOK);
+        const V3 mc = matte_light<Q>(sc, P, N, hit, guardOK, cell, c, r2h);
         sc.probe_end(kProbeMatte);
         tmp = vmul(mc, tmp);
         colour = vadd(tmp, colour);
@@ -1013,7 +1091,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
             r.rd = rd;
             r.ro = vadd(P, vsmul(0.01f, rd));
             r.rI = rc;
-            fr[lv] = r;
+            store_frame_r<IsBvhScene<Scene>::value>(fr[lv], r);
           }
           sc.count(kUDescend, 1);
           ++sp;
@@ -1053,7 +1131,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
         f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
         fc.set(lv, f);
-        const FrameR r = fr[lv];
+        const FrameR r = load_frame_r<IsBvhScene<Scene>::value>(fr[lv]);
         o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 10);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if (Q == 4 && (f.meta & 0x200u)) enterH = originH;  // reflection back into it
@@ -1364,14 +1442,10 @@ struct ListRec {
   float rs, r2, cr, rf;
   int idx;
 };
-// Capsule-list records (sphere_lists, rtg_scene_pack.h): RTG_CAP_WORDS = 4 (the
-// default) {x, y, z, r^2}, four to a 64-byte scalar load, the screen radius^2
-// derived on the device (cap_screen_r2); RTG_CAP_WORDS = 8 (A/B builds) the
-// overlap lists' 32-byte records, two to a load.
-#ifndef RTG_CAP_WORDS
-#define RTG_CAP_WORDS 4
-#endif
-constexpr int kCapWords = RTG_CAP_WORDS;
+// Capsule-list records (sphere_lists, rtg_scene_pack.h): {x, y, z, r^2}, four
+// to a 64-byte scalar load, the screen radius^2 derived on the device
+// (cap_screen_r2).
+constexpr int kCapWords = 4;
 // One capsule-list record (16-byte form, kCapWords == 4): centre and r^2.
 struct CapRec {
   V3 c;
@@ -1597,67 +1671,48 @@ RTG_HD int container_bvh(const Scene& sc, V3 pt) {
 }
 
 // ---------------------------------------------------------------------------
-// Coherent-wave queries of BVH scenes over the sphere lists (sphere_lists,
+// Queries of BVH scenes over the sphere lists (sphere_lists,
 // rtg_scene_pack.h): the n <= 64 masks' sets as lists, walked with a
-// wave-uniform index and one 32-byte scalar record load per sphere, no stack.
-// Taken when every active lane has the same sphere h (most waves of C5:
-// neighbouring samples hit the same sphere), else the BVH.
+// wave-uniform index and scalar record loads, no stack.  The lanes of a wave
+// on one list walk it together; a wave takes its distinct lists in turn (the
+// *_lanes forms), and lanes left after a budget of walks take the BVH.
 
 // Shadow ray from a hit point P of sphere h (guard test passed) to light l:
-// only the spheres of h's capsule list can block it (shadow_masks' argument),
-// and the list holds the likeliest blockers first, so blocked lanes stop early; the
-// wave leaves once every lane is blocked.  Same answer as blocked_bvh: any
+// only the spheres of the capsule list of (l, h, P's cell) can block it
+// (shadow_masks' argument, with the cell's capsule: cell_ball), and the list
+// holds the likeliest blockers first, so blocked lanes stop early; the walk
+// ends once every lane on it is blocked.  Same answer as blocked_bvh: any
 // blocker.
-// The list loops below take records in pairs, k and k + 1, from one 64-byte
-// scalar load (cap_rec2 / ov_rec2), so a wave waits on half as many loads;
-// the second record of a pair past the list's end is not used.
+// The overlap-list loops below take records in pairs, k and k + 1, from one
+// 64-byte scalar load (ov_rec2), so a wave waits on half as many loads; the
+// second record of a pair past the list's end is handled as each says.
 template <class Scene>
-RTG_HD bool blocked_cap(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h) {
+RTG_HD bool blocked_cap(const Scene& sc, const RayQ& q, float gap, unsigned l, int h,
+                        unsigned cell) {
   sc.count(kUQuery, 1);
-  const RayQ q = make_query(o, d);
   unsigned k0, k1;
-  sc.cap_range(l, (unsigned)h, k0, k1);
+  sc.cap_range(l, (unsigned)h, cell, k0, k1);
   bool blk = false;
-  auto step = [&](const ListRec& r) {
-    sc.count(kUCapIter, 1);
-    if (!blk && screen_ahead(q, r.c, r.rs)) {
-      sc.count(kUShdExact, 1);
-      bool res;
-      const float t = ray_sphere_leaf(q, r.c, r.r2, res);
-      take_blocker(t, q.d, gap, blk);
-    }
-  };
-#if RTG_CAP_WORDS == 4
-  // four 16-byte records per 64-byte scalar load; those past the list's end
-  // are the next list's (or the table's padding): a real sphere can only
-  // block if it blocks, so testing it keeps the answer; one exit test per
-  // load
-  for (unsigned k = k0; k < k1; k += 4) {  // wave-uniform
+  // four 16-byte records per 64-byte scalar load, from the list's second
+  // record (its first is h, which blocked_cap_lanes tests for every lane at
+  // once); records past the list's end are the next list's (or the table's
+  // padding): a real sphere can only block if it blocks, so testing it keeps
+  // the answer; one exit test per load
+  for (unsigned k = k0 + 1; k < k1; k += 4) {  // wave-uniform
     CapRec r[4];
     sc.cap_rec4(k, r);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      ListRec e;
-      e.c = r[j].c;
-      e.r2 = r[j].r2;
-      e.rs = cap_screen_r2(r[j].r2);
-      step(e);
+      sc.count(kUCapIter, 1);
+      if (!blk && screen_ahead(q, r[j].c, cap_screen_r2(r[j].r2))) {
+        sc.count(kUShdExact, 1);
+        bool res;
+        const float t = ray_sphere_leaf(q, r[j].c, r[j].r2, res);
+        take_blocker(t, q.d, gap, blk);
+      }
     }
     if (sc.all(blk)) break;
   }
-#else
-  for (unsigned k = k0; k < k1; k += 2) {  // wave-uniform
-    ListRec r0, r1;
-    sc.cap_rec2(k, r0, r1);
-    // the pair's second record past the list's end is the next list's (or
-    // the table's padding record): a real sphere can only block if it
-    // blocks, so testing it keeps the answer; one exit test per pair
-    // 
-    step(r0);
-    step(r1);
-    if (sc.all(blk)) break;
-  }
-#endif
   return blk;
 }
 
@@ -1744,21 +1799,34 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
 // the BVH (the lists' arguments hold per sphere).  A coherent wave is one
 // walk.
 template <class Scene>
-RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h) {
+RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h,
+                              unsigned cell, V3 ch, float r2h) {
+  const RayQ q = make_query(o, d);
+  // h itself (every list's first record: capsule_keep's order key) for every
+  // lane at once, with the lane's own centre and r^2 (the records' values);
+  // the walks then start at each list's second record
+  sc.count(kUShdExact, 1);
+  bool res;
   bool blk = false;
-  bool todo = true;
-  for (int k = 0; k < kListWalks; ++k) {  // wave-uniform
-    const int h0 = sc.lane_with(h, todo);
-    if (todo && h == h0) {
-      // h0 made scalar again inside the branch: the compiler otherwise
-      // substitutes the lane's own h (equal here, but a VGPR) and the walk's
+  take_blocker(ray_sphere_leaf(q, ch, r2h, res), q.d, gap, blk);
+  // walks keyed by (hit sphere, hit-point cell): each key's capsule list
+  // (cap_cell, sphere_lists)
+  const int key = (h << 5) | (int)cell;
+  bool todo = !blk;
+  for (int k = 0; k < kShadowWalks; ++k) {  // wave-uniform
+    if (!sc.any(todo)) return blk;
+    const int k0 = sc.lane_with(key, todo);
+    if (todo && key == k0) {
+      // k0 made scalar again inside the branch: the compiler otherwise
+      // substitutes the lane's own key (equal here, but a VGPR) and the walk's
       // range and record loads become per-lane vector loads
-      blk = blocked_cap(sc, o, d, gap, l, sc.first_lane_i(h0));
+      const int ku = sc.first_lane_i(k0);
+      blk = blocked_cap(sc, q, gap, l, ku >> 5, (unsigned)ku & 31u);
       todo = false;
     }
-    if (!sc.any(todo)) return blk;
   }
-  if (todo) blk = query_blocked<2>(sc, o, d, gap);
+  if (sc.any(todo))
+    if (todo) blk = query_blocked<2>(sc, o, d, gap);
   return blk;
 }
 template <class Scene>

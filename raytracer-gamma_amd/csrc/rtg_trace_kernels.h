@@ -243,9 +243,10 @@ struct DevScene {
     if constexpr (kBvh) return capOff != nullptr;
     else return false;
   }
-  __device__ __forceinline__ void cap_range(unsigned l, unsigned h, unsigned& k0,
+  // capsule list of (light l, sphere h, hit-point cell): one 8-byte scalar load
+  __device__ __forceinline__ void cap_range(unsigned l, unsigned h, unsigned cell, unsigned& k0,
                                             unsigned& k1) const {
-    const cuint_p o = uidx(capOff, l * n + h);
+    const cuint_p o = uidx(capOff, 2u * ((l * n + h) * kCapCells + cell));
     k0 = o[0];
     k1 = o[1];
   }
@@ -283,9 +284,6 @@ struct DevScene {
     r1.cr = g[13];
     r1.idx = __float_as_int(g[14]);
     r1.rf = g[15];
-  }
-  __device__ __forceinline__ void cap_rec2(unsigned k, ListRec& r0, ListRec& r1) const {
-    list_rec2(capRec, k, r0, r1);
   }
   // Capsule records k .. k + 3 (16-byte form) with one 64-byte scalar load.
   __device__ __forceinline__ void cap_rec4(unsigned k, CapRec* r) const {
@@ -459,16 +457,18 @@ struct DevScene {
   // The shading set-up's data of hit sphere i (>= 0): centre, guard radius^2
   // and material.  When every active lane hit the same sphere (a coherent
   // wave) they come through the scalar cache; otherwise per-lane gathers.
-  __device__ __forceinline__ void hit_data(int i, V3& c, float& g2, Mat& mt) const {
+  __device__ __forceinline__ void hit_data(int i, V3& c, float& g2, float& r2, Mat& mt) const {
     const int i0 = __builtin_amdgcn_readfirstlane(i);
     if (__ballot(i != i0) == 0ull) {
       const cfloat_p g = fidx(geom, 4u * (unsigned)i0);
       c = v3(g[0], g[1], g[2]);
+      r2 = g[3];
       g2 = *fidx(crad2, 2 * n + (unsigned)i0);
       mt = mat_at(fidx(mats, 8u * (unsigned)i0));
     } else {
       const cfloat_p g = fidx(geom, 4u * (unsigned)i);
       c = v3(g[0], g[1], g[2]);
+      r2 = g[3];
       g2 = *fidx(crad2, 2 * n + (unsigned)i);
       mt = mat_at(fidx(mats, 8u * (unsigned)i));
     }
@@ -970,7 +970,7 @@ struct GroupsPerWave {
 
 template <int kVariant>
 struct SampleThreads {
-  static constexpr int value = (kVariant == 14) ? kBlock : (kVariant == 16) ? 128 : 64;
+  static constexpr int value = (kVariant == 14) ? kBlock : 64;
 };
 
 // One launch, one pixel group per wave: one-wave workgroups (default), or
@@ -1123,8 +1123,9 @@ void trace_samples_kernel_masked(const KernelArgs a) {
 //     chosen by rtg_context_set_semantics, not by the variant knob)
 //   (19-21, persistent sample kernels with static / atomic-queue dealing of
 //    pixel groups, were removed: register spills made them slower)
-//   16 as 17 with two-wave workgroups
-//   17 as 0 with the materials/geometry staged in LDS per workgroup
+//   (16, 17: as 0 with the materials/geometry staged in LDS per workgroup,
+//    two- and one-wave workgroups; measured slower than the scalar-cache
+//    reads in rounds 1-2 and removed in round 6: DESIGN.md §6)
 //   (10-12: work-queue and workgroup-size trials of the tile kernel, removed: DESIGN.md)
 //   100 + v: diagnostic build of v (s_memtime probes, rtg_diag_read); 100 = 9,
 //     110 = the default sample kernel (0)
@@ -1156,7 +1157,7 @@ constexpr VariantInfo kVariants[] = {
     {1, kVariantTile, false},    {2, kVariantTile, false},    {3, kVariantTile, false},
     {4, kVariantTile, false},    {5, kVariantTile, false},    {6, kVariantTile, false},
     {8, kVariantTile, false},    {14, kVariantSample, false}, {15, kVariantSample, false},
-    {16, kVariantSample, false}, {17, kVariantSample, false}, {18, kVariantSample, false},
+    {18, kVariantSample, false},
     {19, kVariantSample, false}, {20, kVariantSample, false}, {21, kVariantSample, false},
     {22, kVariantSample, false}, {23, kVariantSample, false}, {24, kVariantSample, false},
     {104, kVariantTile, false},  {108, kVariantTile, false},
@@ -1174,7 +1175,7 @@ inline const VariantInfo* variant_info(int v) {
 // request for any other variant gets nullptr, an error, never a wrong frame.
 template <int V>
 struct CompactVariant {
-  static constexpr bool value = V == 0 || V == 15 || V == 17 || V == 18 || V == 19 || V == 20 ||
+  static constexpr bool value = V == 0 || V == 15 || V == 18 || V == 19 || V == 20 ||
                                 V == 23 || V == 24 || V == 50 || V == 110 || V == 120;
 };
 // list: 0 the direct launch, 1 the compacted launch, 2 the compacted launch
@@ -1194,12 +1195,7 @@ static TraceFn trace_fn_v(bool lds, int list) {
     return list == 2 ? trace_samples_kernel<S, false, 120, false, true, true> : nullptr;
   } else if constexpr (V == 110) {  // the probe build of the compacted default kernel
     return list ? trace_samples_kernel<S, false, 110, false, true> : nullptr;
-  } else if constexpr (V == 17) {
-    if (list)
-      return lds ? trace_samples_kernel<S, true, V, false, true>
-                 : trace_samples_kernel<S, false, V, false, true>;
-    return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
-  } else if constexpr (V == 14 || V == 16) {
+  } else if constexpr (V == 14) {
     return lds ? trace_samples_kernel<S, true, V> : trace_samples_kernel<S, false, V>;
   } else if constexpr (CompactVariant<V>::value) {
     return list ? trace_samples_kernel<S, false, V, false, true> : trace_samples_kernel<S, false, V>;

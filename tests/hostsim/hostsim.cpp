@@ -36,9 +36,10 @@ struct HostScene {
   const float* ovRec = nullptr;
   const unsigned* ovOff = nullptr;
   bool has_lists() const { return capOff != nullptr; }
-  void cap_range(unsigned l, unsigned h, unsigned& k0, unsigned& k1) const {
-    k0 = capOff[l * n + h];
-    k1 = capOff[l * n + h + 1];
+  void cap_range(unsigned l, unsigned h, unsigned cell, unsigned& k0, unsigned& k1) const {
+    const size_t slot = ((size_t)l * n + h) * rtg::kCapCells + cell;
+    k0 = capOff[2 * slot];
+    k1 = capOff[2 * slot + 1];
   }
   void ov_range(unsigned h, unsigned& k0, unsigned& k1) const {
     k0 = ovOff[h];
@@ -57,9 +58,6 @@ struct HostScene {
   static void list_rec2(const float* b, unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) {
     r0.c = list_rec(b, k, r0.rs, r0.r2, r0.cr, r0.idx, r0.rf);
     r1.c = list_rec(b, k + 1, r1.rs, r1.r2, r1.cr, r1.idx, r1.rf);
-  }
-  void cap_rec2(unsigned k, rtg::ListRec& r0, rtg::ListRec& r1) const {
-    list_rec2(capRec, k, r0, r1);
   }
   void cap_rec4(unsigned k, rtg::CapRec* r) const {
     for (int j = 0; j < 4; ++j) {
@@ -157,8 +155,7 @@ struct HostScene {
     return r;
   }
   float refr(int i) const { return mats[8 * i + 7]; }
-  void hit_data(int i, rtg::V3& c, float& g2, rtg::Mat& mt) const {
-    float r2;
+  void hit_data(int i, rtg::V3& c, float& g2, float& r2, rtg::Mat& mt) const {
     c = sphere((unsigned)i, r2);
     g2 = guard_r2((unsigned)i);
     mt = mat(i);
@@ -1021,3 +1018,130 @@ extern "C" long hostsim_cap_screen_check(unsigned stride, long* checked) {
   for (uint32_t m = 0; m < 0x800000u; m += 7) one(m);  // subnormals
   return bad;
 }
+
+// The capsule lists' hit-point cells (cap_cell, cell_ball, cell_keep,
+// cell_behind in rtg_scene_pack.h): a sphere left out of the list of cell c
+// of (light l, sphere h) never blocks a shadow ray cast from a hit point P
+// that the kernel classifies into cell c (guard and shell tests passed,
+// incidence > 0), by the reference's own test.  Random scenes at scales
+// 1e-2..1e2; half of the spheres are placed just outside (or on) a random
+// cell capsule of sphere 0 and light 0, and the points P are drawn in that
+// cell near the surface, at the shell's inner radius, near the cell's edges
+// (components near 0, two components of near equal size) and toward the
+// placed spheres.  Returns the violations; *tested counts the (P, sphere)
+// pairs tested.
+extern "C" long hostsim_cell_list_check(long scenes, unsigned n, long points,
+                                        unsigned long long seed, long* tested) {
+  unsigned long long st = seed * 0x9E3779B97F4A7C15ull + 11;
+  auto u01 = [&]() {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    return (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  };
+  long bad = 0, cnt = 0;
+  std::vector<rtg_sphere> sph(n);
+  rtg_light lg[2];
+  for (long sc = 0; sc < scenes; ++sc) {
+    const double scale = pow(10.0, -2.0 + 4.0 * u01());
+    for (unsigned i = 0; i < n; ++i) {
+      memset(&sph[i], 0, sizeof(rtg_sphere));
+      sph[i].pos.x = (float)((u01() - 0.5) * 24 * scale);
+      sph[i].pos.y = (float)((u01() - 0.5) * 16 * scale);
+      sph[i].pos.z = (float)((-6 - 34 * u01()) * scale);
+      sph[i].radius = (float)((0.3 + 3 * u01()) * scale);
+    }
+    for (int l = 0; l < 2; ++l) {
+      lg[l].pos.x = (float)((u01() - 0.5) * 120 * scale);
+      lg[l].pos.y = (float)((10 + 70 * u01()) * scale);
+      lg[l].pos.z = (float)((u01() - 0.5) * 130 * scale);
+    }
+    const double L0[3] = {lg[0].pos.x, lg[0].pos.y, lg[0].pos.z};
+    const unsigned c0 = (unsigned)(u01() * 24) % 24;
+    double b0[3], rho0;
+    rtg::cell_ball(sph[0], c0, b0, &rho0);
+    for (unsigned i = n / 2; i < n; ++i) {  // just outside cell c0's capsule
+      const double t = (i & 1) ? u01() : 0.05 * u01() * u01();
+      double p[3], ab[3];
+      for (int k = 0; k < 3; ++k) { ab[k] = L0[k] - b0[k]; p[k] = b0[k] + t * ab[k]; }
+      double v[3] = {u01() - 0.5, u01() - 0.5, u01() - 0.5};
+      const double ab2 = ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2];
+      const double pr = (v[0] * ab[0] + v[1] * ab[1] + v[2] * ab[2]) / ab2;
+      for (int k = 0; k < 3; ++k) v[k] -= pr * ab[k];
+      const double vl = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      const double ri = sph[i].radius;
+      const double dist = (rho0 + ri) * (1.0 + (u01() < 0.3 ? -0.1 : 1.0) * pow(10.0, -4.0 + 2.5 * u01()));
+      sph[i].pos.x = (float)(p[0] + dist * v[0] / vl);
+      sph[i].pos.y = (float)(p[1] + dist * v[1] / vl);
+      sph[i].pos.z = (float)(p[2] + dist * v[2] / vl);
+    }
+    for (int l = 0; l < 2; ++l) {
+      const double L[3] = {lg[l].pos.x, lg[l].pos.y, lg[l].pos.z};
+      for (unsigned h = 0; h < (l == 0 ? 4u : 2u); ++h) {
+        const rtg_sphere& sh = sph[h];
+        const float G2 = rtg::guard_r2(sh);
+        const float r2h = sh.radius * sh.radius;
+        const double rh = fabs((double)sh.radius);
+        for (unsigned cell = 0; cell < rtg::kCapCubeCells; ++cell) {
+          if (h == 0 && l == 0 && cell != c0 && u01() < 0.7) continue;
+          const bool shared = rtg::cell_behind(sh, cell, L);
+          double b[3], rho;
+          rtg::cell_ball(sh, cell, b, &rho);
+          const unsigned a = cell >> 3, pa = a == 0 ? 1 : 0, qa = a == 2 ? 1 : 2;
+          const double sa = (cell & 4) ? -1.0 : 1.0, sp = (cell & 2) ? -1.0 : 1.0,
+                       sq = (cell & 1) ? -1.0 : 1.0;
+          for (unsigned i = 0; i < n; ++i) {
+            if (rtg::capsule_keep(sph.data(), h, i, L) &&
+                (shared || rtg::cell_keep(sph.data(), h, i, L, b, rho)))
+              continue;  // in the cell's list
+            for (long k = 0; k < points; ++k) {
+              // a direction in the cell: gnomonic coordinates in [0, 1]^2,
+              // often at an edge (0 or 1), or toward sphere i
+              double pp = u01(), qq = u01();
+              const int edge = (int)(k % 5);
+              if (edge == 1) pp = pow(10.0, -9.0 * u01());
+              if (edge == 2) qq = 1.0 - pow(10.0, -9.0 * u01());
+              if (edge == 3) { pp = 1.0 - pow(10.0, -8.0 * u01()); qq = pow(10.0, -8.0 * u01()); }
+              double u[3];
+              u[a] = sa; u[pa] = sp * pp; u[qa] = sq * qq;
+              if (edge == 4) {  // toward sphere i (clamped into the cell)
+                double cv[3] = {(double)sph[i].pos.x - sh.pos.x, (double)sph[i].pos.y - sh.pos.y,
+                                (double)sph[i].pos.z - sh.pos.z};
+                const double ca = fabs(cv[a]) + 1e-300;
+                double p2 = sp * cv[pa] / ca, q2 = sq * cv[qa] / ca;
+                p2 = p2 < 0 ? 0 : (p2 > 1 ? 1 : p2);
+                q2 = q2 < 0 ? 0 : (q2 > 1 ? 1 : q2);
+                u[pa] = sp * p2; u[qa] = sq * q2;
+              }
+              const double ul = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+              const double rad = (k % 7 == 0) ? rh * (1.0 - 0x1p-8) * (1.0 + (u01() - 0.5) * 1e-6)
+                                               : rh * (1.0 + (u01() - 0.7) * 2e-3);
+              const rtg::V3 P = rtg::v3((float)(sh.pos.x + rad * u[0] / ul),
+                                        (float)(sh.pos.y + rad * u[1] / ul),
+                                        (float)(sh.pos.z + rad * u[2] / ul));
+              const rtg::V3 e = rtg::vsub(P, rtg::v3(sh.pos.x, sh.pos.y, sh.pos.z));
+              if (!(rtg::vdot(e, e) <= G2)) continue;
+              if (rtg::cap_cell(e, r2h) != cell) continue;  // another cell's list serves it
+              const rtg::V3 Lp = rtg::v3(lg[l].pos.x, lg[l].pos.y, lg[l].pos.z);
+              const rtg::V3 dist = rtg::vsub(Lp, P);
+              const float gap = rtg::vdot(dist, dist);
+              const rtg::V3 D = rtg::vsmul(1.f / sqrtf(gap), dist);
+              const rtg::V3 N = rtg::vnorm(e);
+              if (!(rtg::vdot(N, D) > 0.f)) continue;
+              const rtg::RayQ q = rtg::make_query(P, D);
+              ++cnt;
+              bool res;
+              const float t = rtg::ray_sphere(q, rtg::v3(sph[i].pos.x, sph[i].pos.y, sph[i].pos.z),
+                                              sph[i].radius * sph[i].radius, res);
+              if (res && t < 1000.f) {
+                const rtg::V3 tv = rtg::vsmul(t, D);
+                if (rtg::vdot(tv, tv) < gap) ++bad;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  if (tested) *tested = cnt;
+  return bad;
+}
+extern "C" void hostsim_cell_ball_slack(double s) { rtg::g_cellBallSlack = s; }

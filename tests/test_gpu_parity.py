@@ -21,7 +21,7 @@ ALL = ["ref800", "c1", "c2", "c3", "c4", "c5"]
 # Kernel variants of the shipped librtg.so (rtg_trace_kernels.h kVariants);
 # the A/B variants exist only in `make AB=1` builds (test_ab_variants).
 SHIPPED = [0, 9, 100, 110, 120]
-AB_VARIANTS = [1, 2, 3, 4, 5, 6, 8, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 104, 108]
+AB_VARIANTS = [1, 2, 3, 4, 5, 6, 8, 14, 15, 18, 19, 20, 21, 22, 23, 24, 104, 108]
 
 
 @pytest.fixture(scope="module")

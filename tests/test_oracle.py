@@ -285,6 +285,31 @@ def test_shadow_masks_are_conservative(hostsim):
         hostsim.hostsim_capsule_back_slack(0.0)
 
 
+def test_cell_lists_are_conservative(hostsim):
+    """A sphere left out of the capsule list of a hit-point cell (cap_cell,
+    cell_ball, cell_keep, cell_behind: rtg_scene_pack.h, the BVH scenes'
+    shadow lists) never blocks a shadow ray from a point the kernel puts in
+    that cell, by the reference's own test: random scenes at scales
+    1e-2..1e2, half of the spheres just outside one cell's capsule, points
+    near the surface, at the shell's inner radius, at the cells' edges and
+    toward the left-out spheres, incidence > 0.  Shrinking the cell balls by
+    1/8 finds blockers."""
+    f = hostsim.hostsim_cell_list_check
+    f.restype = ctypes.c_long
+    hostsim.hostsim_cell_ball_slack.argtypes = [ctypes.c_double]
+    tested = ctypes.c_long(0)
+    bad = f(ctypes.c_long(300), 12, ctypes.c_long(40), ctypes.c_ulonglong(7),
+            ctypes.byref(tested))
+    assert bad == 0, bad
+    assert tested.value > 300_000, tested.value
+    try:
+        hostsim.hostsim_cell_ball_slack(0.125)
+        assert f(ctypes.c_long(300), 12, ctypes.c_long(40), ctypes.c_ulonglong(8),
+                 ctypes.byref(tested)) > 0  # the check has teeth
+    finally:
+        hostsim.hostsim_cell_ball_slack(0.0)
+
+
 @pytest.mark.parametrize("name", ["c2", "c3", "c4"])
 def test_shadow_masks_cull(hostsim, golden, name):
     """The masks of the benchmark scenes are small (the point of them)."""

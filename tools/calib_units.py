@@ -14,7 +14,10 @@ CPU part (`--fit DIR`): solves for unit costs c >= 0 minimising the relative
 residuals of  sum_u waves[k, u] c_u  against SQ_INSTS_VALU[k], with a ridge
 toward the source-priced costs (so units the scene set does not separate keep
 their prices), and prints the fitted table and the per-scene residuals before
-and after.
+and after, plus held-out ratios for the bench configs (each left out of its
+own fit; and a fit on the seeded scenes alone).  The prior and the 0.6-1.7x
+bounds are always the source prices (work.py UNIT_COST_SOURCE), so a refit
+never starts from an earlier fit.
 
   rocprofv3 --pmc SQ_INSTS_VALU --output-format csv -d OUT -o run -- \\
       python3 tools/calib_units.py --collect OUT
@@ -109,37 +112,62 @@ def load_pmc(d):
     return [v for _, v in rows]
 
 
-def fit(d, lam):
+def solve(A, y, wgt, c0, lam):
+    """Unit costs c in [0.6, 1.7] x c0 minimising the weighted relative
+    residuals of A c against y, with a ridge (relative) toward c0."""
     from scipy.optimize import lsq_linear
-    from rtg_amd.work import UNIT_COST
+    Ar = A / y[:, None] * wgt[:, None]
+    reg = np.sqrt(lam) * np.diag(1.0 / c0)
+    M = np.vstack([Ar, reg])
+    b = np.concatenate([wgt, np.sqrt(lam) * np.ones(len(c0))])
+    return lsq_linear(M, b, bounds=(0.6 * c0, 1.7 * c0)).x
+
+
+def fit(d, lam):
+    # The prior and the bounds are the SOURCE prices (rtg_amd/work.py
+    # UNIT_COST_SOURCE), never a previous fit's, so refits do not drift.
+    from rtg_amd.work import UNIT_COST_SOURCE
+    bench = ("c2", "c3", "c4", "c5")
     rec = json.load(open(os.path.join(d, "scenes.json")))
     y = np.array(load_pmc(d))
     assert len(y) == len(rec), (len(y), len(rec))
-    units = [u for u in UNIT_COST if any(r["waves"].get(u, 0) for r in rec)]
+    units = [u for u in UNIT_COST_SOURCE if any(r["waves"].get(u, 0) for r in rec)]
     A = np.array([[r["waves"].get(u, 0) for u in units] for r in rec], float)
-    c0 = np.array([UNIT_COST[u] for u in units], float)
-    # relative residuals, the bench configs weighted 10x; ridge (relative) toward c0
-    wgt = np.array([10.0 if r["scene"] in ("c2", "c3", "c4", "c5") else 1.0 for r in rec])
-    Ar = A / y[:, None] * wgt[:, None]
-    br = wgt
-    reg = np.sqrt(lam) * np.diag(1.0 / c0)
-    M = np.vstack([Ar, reg])
-    b = np.concatenate([br, np.sqrt(lam) * np.ones(len(c0))])
-    sol = lsq_linear(M, b, bounds=(0.6 * c0, 1.7 * c0))
-    c = sol.x
+    c0 = np.array([UNIT_COST_SOURCE[u] for u in units], float)
+    # relative residuals, the bench configs weighted 10x
+    isb = np.array([r["scene"] in bench for r in rec])
+    wgt = np.where(isb, 10.0, 1.0)
+    c = solve(A, y, wgt, c0, lam)
     before, after = A @ c0 / y, A @ c / y
-    print(f"{'scene':8s} {'PMC VALU':>12s} {'model/PMC before':>17s} {'after':>8s}")
-    for r, yy, b0, a0 in zip(rec, y, before, after):
-        print(f"{r['scene']:8s} {yy:12.4g} {b0:17.4f} {a0:8.4f}")
-    print(f"rms rel. error before {np.sqrt(np.mean((before - 1) ** 2)):.4f} "
-          f"after {np.sqrt(np.mean((after - 1) ** 2)):.4f}")
-    print("unit costs (source-priced -> fitted):")
+    # held-out figures: each bench config left out of its own fit, and a fit
+    # without any bench config (the seeded scenes only)
+    loo = {}
+    for k, r in enumerate(rec):
+        if r["scene"] in bench:
+            keep = np.arange(len(rec)) != k
+            ck = solve(A[keep], y[keep], wgt[keep], c0, lam)
+            loo[r["scene"]] = float(A[k] @ ck / y[k])
+    cn = solve(A[~isb], y[~isb], wgt[~isb], c0, lam)
+    nob = {r["scene"]: float(A[k] @ cn / y[k]) for k, r in enumerate(rec) if r["scene"] in bench}
+    print(f"{'scene':8s} {'PMC VALU':>12s} {'source/PMC':>11s} {'fitted':>8s} {'held out':>9s}")
+    for k, (r, yy, b0, a0) in enumerate(zip(rec, y, before, after)):
+        ho = f"{loo[r['scene']]:9.4f}" if r["scene"] in loo else ""
+        print(f"{r['scene']:8s} {yy:12.4g} {b0:11.4f} {a0:8.4f} {ho}")
+    print(f"rms rel. error: source prices {np.sqrt(np.mean((before - 1) ** 2)):.4f}, "
+          f"fitted (in sample) {np.sqrt(np.mean((after - 1) ** 2)):.4f}")
+    print("held out, each bench config left out of its own fit: " +
+          ", ".join(f"{k} {v:.4f}" for k, v in loo.items()))
+    print("held out, fit without any bench config: " +
+          ", ".join(f"{k} {v:.4f}" for k, v in nob.items()))
+    print("unit costs (source price -> fitted, bounds 0.6-1.7x the source price):")
     out = {}
     for u, a, b2 in zip(units, c0, c):
         out[u] = round(float(b2), 2)
         print(f"  {u:14s} {a:6.1f} -> {b2:7.2f}")
-    json.dump({"lambda": lam, "costs": out, "rms_before": float(np.sqrt(np.mean((before - 1) ** 2))),
-               "rms_after": float(np.sqrt(np.mean((after - 1) ** 2)))},
+    json.dump({"lambda": lam, "costs": out, "prior": "UNIT_COST_SOURCE",
+               "rms_before": float(np.sqrt(np.mean((before - 1) ** 2))),
+               "rms_after": float(np.sqrt(np.mean((after - 1) ** 2))),
+               "held_out_leave_one_config": loo, "held_out_no_bench_configs": nob},
               open(os.path.join(d, "fit.json"), "w"), indent=1)
 
 
