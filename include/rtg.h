@@ -127,7 +127,13 @@ int rtg_multi_destroy(rtg_multi* mg);
 #define RTG_GATHER_PEER_COPY 1
 int rtg_multi_set_gather(rtg_multi* mg, int mode);
 
-/* ---- persistent context: scene resident in HBM, caller-owned streams ---- */
+/* ---- persistent context: scene resident in HBM, caller-owned streams ----
+ * A context may render on several streams; it orders its own scratch between
+ * them with events (a launch on a stream other than the one its scratch slot
+ * last ran on waits for that launch; hipStreamPerThread always waits).  A
+ * stream handle that is destroyed and recreated while renders of the context
+ * are still pending on it may come back with the same value: synchronise
+ * such a stream (or the device) before destroying it. */
 typedef struct rtg_context rtg_context;
 int rtg_context_create(int device, rtg_context** out);
 int rtg_context_destroy(rtg_context* ctx);

@@ -356,8 +356,13 @@ struct rtg_context {
   int persistPerCU = 0;  // > 0: fixed persistent waves per CU (RTG_PERSIST_PER_CU A/B knob)
   int lptMin = 2;        // heavy-first listing threshold (cull_groups_kernel; RTG_LPT_MIN A/B knob)
   size_t timelineCap = 0, timelineCount = 0;
-  size_t lastGroups = 0;  // pixel groups of the last compacted launch (rtg_diag_group_list)
-  size_t lastPartCap = 0;  // and its list partitions' capacity (KernelArgs::groupCap)
+  // The last committed compacted launch (rtg_diag_group_list): its slot,
+  // pixel groups, list partitions' capacity (KernelArgs::groupCap) and cost
+  // entry (or -1), all set at the launch's commit point only.
+  int lastSlot = -1;
+  size_t lastGroups = 0;
+  size_t lastPartCap = 0;
+  int lastCost = -1;
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
   bool hasScene = false;
@@ -573,8 +578,11 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
   DeviceGuard deviceGuard;  // the caller's current device is restored on return
   rtg_clear_error();
   if (!ctx || !groups) return RTG_ERR_INVALID;
-  const rtg_context::GroupSlot& slot =
-      ctx->slots[(ctx->nextSlot + rtg_context::kSlots - 1) % rtg_context::kSlots];
+  if (ctx->lastSlot < 0) {
+    rtg_set_error("rtg_diag_group_list: no compacted launch yet");
+    return RTG_ERR_INVALID;
+  }
+  const rtg_context::GroupSlot& slot = ctx->slots[ctx->lastSlot];
   if (!slot.count || !slot.list) {
     rtg_set_error("rtg_diag_group_list: no compacted launch yet");
     return RTG_ERR_INVALID;
@@ -584,10 +592,9 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipDeviceSynchronize());
   if (cost) {
-    const rtg_context::CostEntry* ce = nullptr;
-    for (const auto& e : ctx->costs)
-      if (e.launches && e.cost && (!ce || e.lastUse > ce->lastUse)) ce = &e;
-    if (ce && ce->cap >= k) HIP_TRY(hipMemcpy(cost, ce->cost, k * sizeof(unsigned), hipMemcpyDeviceToHost));
+    // the last launch's own entry (none: the feedback was off for it)
+    const rtg_context::CostEntry* ce = ctx->lastCost >= 0 ? &ctx->costs[ctx->lastCost] : nullptr;
+    if (ce && ce->cost && ce->cap >= k) HIP_TRY(hipMemcpy(cost, ce->cost, k * sizeof(unsigned), hipMemcpyDeviceToHost));
     else memset(cost, 0, k * sizeof(unsigned));
   }
   if (!list && !sel && !runs) return RTG_OK;
@@ -943,14 +950,17 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     if (compact && ctx->n <= 64 && listCap < 0xFFFFFFFFull) {
       listed = true;
       const hipStream_t st = (hipStream_t)stream;
-      slotIdx = ctx->nextSlot;
+      slotIdx = ctx->nextSlot;  // the ring advances at the commit below
       slot = &ctx->slots[slotIdx];
-      ctx->nextSlot = (ctx->nextSlot + 1) % rtg_context::kSlots;
       if (!slot->done)
         HIP_TRY(hipEventCreateWithFlags(&slot->done,
                                         hipEventDisableTiming | hipEventDisableSystemFence));
-      else if (slot->stream != st)
-        HIP_TRY(hipStreamWaitEvent(st, slot->done, 0));  // the slot's last launch
+      else if (slot->stream != st || st == hipStreamPerThread)
+        // the slot's last launch; the per-thread default stream's handle names
+        // a different stream in each host thread, so it always waits (a
+        // context must not span a stream handle destroyed and reused while
+        // its launches are pending: rtg.h)
+        HIP_TRY(hipStreamWaitEvent(st, slot->done, 0));
       if (slot->cap < listCap) {
         // stream-ordered: freed after the slot's last kernel (waited on above)
         if (slot->list) HIP_TRY(hipFreeAsync(slot->list, st));
@@ -982,7 +992,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
             if (e.lastUse < ce->lastUse) ce = &e;
           // the replaced entry's buffers may still be read by queued launches
           // (any stream): this stream waits for its last one
-          if (ce->slot >= 0 && ce->stream != st)
+          if (ce->slot >= 0 && (ce->stream != st || st == hipStreamPerThread))
             HIP_TRY(hipStreamWaitEvent(st, ctx->slots[ce->slot].done, 0));
           ce->key = 0;
           ce->launches = 0;
@@ -1001,7 +1011,8 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
         } else {
           // launches of this entry on other streams may still add to or zero
           // its sums: this stream waits for the last one
-          if (ce->stream != st) HIP_TRY(hipStreamWaitEvent(st, ctx->slots[ce->slot].done, 0));
+          if (ce->stream != st || st == hipStreamPerThread)
+            HIP_TRY(hipStreamWaitEvent(st, ctx->slots[ce->slot].done, 0));
         }
         // the trace kernel writes groupCost every launch; the cull pass reads
         // it (and sums it into costStat) once a launch has written it, and
@@ -1028,8 +1039,6 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       a.groupCount = slot->count + kCountSet * slot->parity;
       a.zeroCount = slot->count + kCountSet * (1 - slot->parity);  // parity flips at the commit
       a.groupCap = (unsigned)partCap;
-      ctx->lastGroups = groups;
-      ctx->lastPartCap = partCap;
       // a multiple of kListParts (wave w takes list partition w % kListParts)
       const size_t np = groups < persist ? groups : persist;
       a.nPersist = (unsigned)((np + kListParts - 1) / kListParts * kListParts);
@@ -1069,7 +1078,14 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   // and the cost entry advance only now (an earlier error return leaves both
   // as the previous launch left them: its trace kernel zeroed exactly the set
   // this launch would have used).
-  if (slot) slot->parity ^= 1u;
+  if (slot) {
+    slot->parity ^= 1u;
+    ctx->nextSlot = (slotIdx + 1) % rtg_context::kSlots;
+    ctx->lastSlot = slotIdx;
+    ctx->lastGroups = cullGroups;
+    ctx->lastPartCap = a.groupCap;
+    ctx->lastCost = costEntry ? (int)(costEntry - ctx->costs) : -1;
+  }
   if (costEntry) {
     costEntry->slot = slotIdx;
     costEntry->stream = (hipStream_t)stream;

@@ -919,6 +919,9 @@ RTG_HD FrameR load_frame_r(const FrameR& src) {
   return src;
 }
 
+#ifndef RTG_BVH_INSIDE  // A/B: internal reflections of BVH scenes as entering rays
+#define RTG_BVH_INSIDE 0
+#endif
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
 // kCL: the reference OpenCL kernel's semantics (raytrace_kernel.cl:641-867):
@@ -1080,6 +1083,16 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           const bool inside = Q == 4 && origin && vdot(d, N) > 0.f;
           f.meta = ((unsigned)rm << 10) | (inside ? 0x200u : 0u) |
                    ((unsigned)(origin ? hit + 1 : 0) << 2) | (sigR ? 2u : 0u);
+#if RTG_BVH_INSIDE
+          if constexpr (Q == 4 && IsBvhScene<Scene>::value) {
+            // BVH scenes below 2048 spheres: the same for the sphere lists
+            // (closest_enter_list), the sphere in bits 10..20 and rm in 21..31
+            const bool in = sc.n < 2048u && guardOK && vdot(d, N) > 0.f;
+            if (sc.n < 2048u)
+              f.meta = ((unsigned)rm << 21) | ((unsigned)(in ? hit + 1 : 0) << 10) |
+                       (in ? 0x200u : 0u) | (sigR ? 2u : 0u);
+          }
+#endif
           fc.set(lv, f);
           if (sigR) {
             sc.count(kCntReflPush, 1);
@@ -1135,6 +1148,15 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 10);
         originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
         if (Q == 4 && (f.meta & 0x200u)) enterH = originH;  // reflection back into it
+#if RTG_BVH_INSIDE
+        if constexpr (Q == 4 && IsBvhScene<Scene>::value) {
+          if (sc.n < 2048u) {
+            rm = (int)(f.meta >> 21);
+            originH = -1;
+            enterH = (f.meta & 0x200u) ? (int)((f.meta >> 10) & 0x7FFu) - 1 : -1;
+          }
+        }
+#endif
         if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
         descend = true;
         break;
