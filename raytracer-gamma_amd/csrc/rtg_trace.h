@@ -919,8 +919,11 @@ RTG_HD FrameR load_frame_r(const FrameR& src) {
   return src;
 }
 
-#ifndef RTG_BVH_INSIDE  // A/B: internal reflections of BVH scenes as entering rays
-#define RTG_BVH_INSIDE 0
+// Internal reflections of BVH scenes traced as entering rays (the sphere in
+// the frame record, scenes below 2048 spheres): C5 -3.3 %, DESIGN.md §4
+// item 63.  0 in A/B builds only.
+#ifndef RTG_BVH_INSIDE
+#define RTG_BVH_INSIDE 1
 #endif
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).

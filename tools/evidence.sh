@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
-# tools/r05_evidence.sh — the round-5 evidence set in one GPU call, on the
-# final sources: GPU tests + smoke, the PMC passes of C3, C2 and C5 (their
+# tools/evidence.sh — a round's evidence set in one GPU call (TAG, default
+# r06), on the final sources: GPU tests + smoke, the PMC passes of C3, C2, C4
+# and C5 (their
 # records go to profiles/pmc_<config>.json, which bench.py matches by source
 # hash), the bench line of every config (C1 as the CPU-only line), and the
 # rocprofv3 kernel trace of the C3 / C2 / C5 bench commands cut to their timed
@@ -8,7 +9,7 @@
 # chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 if [ -z "$SKIP_TESTS" ]; then
@@ -17,7 +18,7 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && tail -1 $OUT/smoke.log || exit 1
 fi
 if [ -z "$NO_PMC" ]; then
-  for c in ${PMC_CONFIGS:-c3 c2 c5}; do
+  for c in ${PMC_CONFIGS:-c3 c2 c4 c5}; do
     steps=3; [ "$c" = c5 ] && steps=1
     echo "== PMC $c" &&
     TAG=${TAG}_$c CFG=$c ARGS="--config $c --steps $steps --warmup 1 --no-cpu-baseline --no-work-count --no-e2e" \

@@ -8,6 +8,8 @@
 #   tests                         the GPU test tier
 #   bench:CFG[:EXTRA_ARGS]        one default bench line (the shipped library)
 #   prof:CFG                      rocprofv3 --kernel-trace --stats of a bench run
+#   calib                         unit-cost calibration data (tools/calib_units.py --collect)
+#   chunks:CFG[:RANKS[:CHUNKS]]   one rank's chunked shard (tools/chunk_rehearsal.py)
 # Replaces round 5's per-call wrappers (tools/r05*_call.sh).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -38,6 +40,16 @@ for step in "$@"; do
           --output-format csv -d "$d" -o run -- python3 "$ROOT/bench.py" --config "$a" --steps 1 --warmup 1 \
           --no-cpu-baseline --no-work-count --no-e2e > "$d.json" 2> "$d.err" ) || { tail -5 "$d.err"; exit 1; }
       python3 tools/pmc_kernel_avg.py "$d" "$d.json" | tee "$d.txt" ;;
+    calib)
+      # tools/calib_units.py --collect under the SQ_INSTS_VALU counter
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 600 rocprofv3 --pmc SQ_INSTS_VALU --output-format csv \
+          -d "$O/calib" -o run -- python3 "$ROOT/tools/calib_units.py" --collect "$O/calib" > "$O/calib.log" 2>&1 ) \
+        || { tail -20 "$O/calib.log"; exit 1; }
+      tail -3 "$O/calib.log" ;;
+    chunks)
+      timeout -k 10 300 python tools/chunk_rehearsal.py --config "$a" --ranks "${b:-8,4,2}" --chunks "${c:-1,3,4}" \
+        --last-frac 0.15 --steps 20 --json "$O/chunks_$a.json" > "$O/chunks_$a.txt" 2>&1 || { tail -5 "$O/chunks_$a.txt"; exit 1; }
+      cat "$O/chunks_$a.txt" | grep config ;;
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         > "$O/pytest_gpu.log" 2>&1 || { tail -40 "$O/pytest_gpu.log"; exit 1; }
