@@ -881,7 +881,7 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
 // The reflection-child records in private memory (trace_sample's fr[]):
 // BVH scenes (C5: S = 8, 54 GB of record traffic per frame) store and load
 // them with the nontemporal (streaming) policy, so they do not push the scene's
-// node and list lines out of the caches: C5 -1 to -1.2 % (DESIGN.md §4 item 61);
+// node and list lines out of the caches: C5 -1 to -1.2 % (DESIGN.md §4 item 62);
 // the masked scenes keep the default policy (C3 +7.5 %, C4 +6.6 % with it:
 // their records are re-read while still cached).
 template <bool kNT>
@@ -1722,7 +1722,7 @@ RTG_HD bool blocked_cap(const Scene& sc, const RayQ& q, float gap, unsigned l, i
   // record (its first is h, which blocked_cap_lanes tests for every lane at
   // once); records past the list's end are the next list's (or the table's
   // padding): a real sphere can only block if it blocks, so testing it keeps
-  // the answer; one exit test per load (DESIGN.md §4 items 47, 59)
+  // the answer; one exit test per load (DESIGN.md §4 items 47, 60)
   for (unsigned k = k0 + 1; k < k1; k += 4) {  // wave-uniform
     CapRec r[4];
     sc.cap_rec4(k, r);

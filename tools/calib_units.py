@@ -22,7 +22,7 @@ never starts from an earlier fit.
   rocprofv3 --pmc SQ_INSTS_VALU --output-format csv -d OUT -o run -- \\
       python3 tools/calib_units.py --collect OUT
   python3 tools/calib_units.py --fit OUT
-  python3 tools/calib_units.py --fit profiles/r05/calib_units   # the committed data
+  python3 tools/calib_units.py --fit profiles/r06/calib_units   # the committed data
 """
 import argparse
 import csv
@@ -91,7 +91,7 @@ def collect(out_dir):
 
 def load_pmc(d):
     rows = []
-    js = os.path.join(d, "pmc.json")  # the committed form (profiles/r05/calib_units/)
+    js = os.path.join(d, "pmc.json")  # the committed form (profiles/r06/calib_units/)
     if os.path.exists(js):
         for r in json.load(open(js)):
             nm = r["kernel"]
