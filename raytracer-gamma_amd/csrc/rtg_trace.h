@@ -608,7 +608,8 @@ RTG_HD int query_closest(const Scene& sc, V3 o, V3 d, float& t);
 template <int Q, class Scene>
 RTG_HD bool query_blocked(const Scene& sc, V3 o, V3 d, float gap);
 template <class Scene>
-RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel);
+RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel, int hit = -1,
+                        V3 hc = V3{}, float hr2 = 0.f);
 template <class Scene>
 RTG_HD bool blocked_cap(const Scene& sc, const RayQ& q, float gap, unsigned l, int h,
                         unsigned cell);
@@ -685,7 +686,7 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
           const uint64_t su = sc.shadow_union(l, hit, guardOK);
           sc.count(kCntShadowQ, 1);
           sc.count(kCntShadowSel, __builtin_popcountll(su));
-          blk = blocked_sel(sc, P, dir, gap, su);
+          blk = blocked_sel(sc, P, dir, gap, su, hit, hc, hr2);
         } else if (sc.has_lists() && sc.all(guardOK)) {
           // BVH scene: each lane's hit sphere's capsule list for light l, the
           // wave's distinct hit spheres in turn (blocked_cap_lanes)
@@ -924,6 +925,9 @@ RTG_HD FrameR load_frame_r(const FrameR& src) {
 // item 63.  0 in A/B builds only.
 #ifndef RTG_BVH_INSIDE
 #define RTG_BVH_INSIDE 1
+#endif
+#ifndef RTG_SELF_SKIP  // the masked scenes' shadow self test (blocked_sel); 0: A/B builds
+#define RTG_SELF_SKIP 1
 #endif
 // One primary sample: rayTrace(spheres, ..., ray, bgMaterial, 0),
 // raytracer.h:410-636, for stack capacity S (RTSTACK_MAXSIZE).
@@ -1964,7 +1968,8 @@ RTG_HD unsigned sign_mask(float v) {
 // second loop), and the wave leaves once every lane is blocked.  Same answer:
 // blocked iff any sphere of `sel` blocks.
 template <bool kFast, class Scene>
-RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_t sel) {
+RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_t sel,
+                              int skip = -1) {
   bool blk = false;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
@@ -1972,7 +1977,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
     sc.count(kUShdIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
-    if (!blk && !(pass1_rad(q, c, rs) < 0.f)) {
+    if (!blk && (int)i != skip && !(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntShadowCand, 1);
       sc.count(kUShdExact, 1);
       bool res;
@@ -1988,13 +1993,34 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
 }
 
 template <class Scene>
-RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel) {
+RTG_HD bool blocked_sel(const Scene& sc, V3 o, V3 d, float gap, uint64_t sel, int hit,
+                        V3 hc, float hr2) {
   sc.count(kUQuery, 1);
   const RayQ q = make_query(o, d);
   if (sc.fuse & kFuseShadow) {
-    if (sc.all(q.fast)) return blocked_sel_fused<true>(sc, q, gap, sel);
-    return blocked_sel_fused<false>(sc, q, gap, sel);
+    // The hit sphere itself (every shadow mask's own sphere): no_root on the
+    // reference's own b and cc for it (ray_sphere's operations on the same
+    // centre and r^2) shows for all but grazing rays that it accepts no root,
+    // so it cannot block; those lanes skip it, and a wave whose lanes all hit
+    // one sphere and all show it drops the sphere from the loop (DESIGN.md §4
+    // item 64).
+    int skip = -1;
+#if RTG_SELF_SKIP
+    if (hit >= 0) {
+      const V3 e = vsub(q.o, hc);
+      const float b = 2.0f * vdot(q.d, e);
+      const float cc = vdot(e, e) - hr2;
+      if (no_root(q, b, cc)) skip = hit;
+      const int h0 = sc.first_lane_i(hit);
+      if (sc.all(skip == h0)) sel &= ~(1ull << h0);
+    }
+#else
+    (void)hit; (void)hc; (void)hr2;
+#endif
+    if (sc.all(q.fast)) return blocked_sel_fused<true>(sc, q, gap, sel, skip);
+    return blocked_sel_fused<false>(sc, q, gap, sel, skip);
   }
+  (void)hit; (void)hc; (void)hr2;
   for (unsigned base = 0; base < 64u; base += 32u) {
     const unsigned u = (unsigned)(sel >> base);
     unsigned cand = 0;
