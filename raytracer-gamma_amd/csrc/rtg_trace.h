@@ -981,11 +981,28 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       const float cu = vdot(dh, U);
       const int tier = sc.all(cu >= kConeCos[0]) ? 0 : sc.all(cu >= kConeCos[1]) ? 1 : -1;
       if (tier >= 0) {
-        const uint64_t cm = sc.cone_union(originH, (unsigned)tier, (unsigned)cone_cell(U));
+        uint64_t cm = sc.cone_union(originH, (unsigned)tier, (unsigned)cone_cell(U));
+        const RayQ q = make_query(o, d);
+        int skip = -1;
+#if RTG_SELF_SKIP
+        {
+          // the origin sphere (in every cone mask of its own): a ray leaving
+          // its surface (refraction out of it) or starting 0.01 off it
+          // (reflection) accepts no root of it when no_root holds on the
+          // reference's own b and cc (ray_sphere's operations), so those lanes
+          // skip it; a wave whose lanes share it and all show it drops it
+          float r2o, g2o;
+          const V3 co = sc.sphere_guard(originH, r2o, g2o);
+          const V3 e = vsub(q.o, co);
+          if (no_root(q, 2.0f * vdot(q.d, e), vdot(e, e) - r2o)) skip = originH;
+          const int h0 = sc.first_lane_i(originH);
+          if (sc.all(skip == h0)) cm &= ~(1ull << h0);
+        }
+#endif
         sc.count(kCntConeQ, 1);
         sc.count(kCntConeSel, __builtin_popcountll(cm));
         sc.count(kUQuery, 1);
-        hit = closest_sel(sc, make_query(o, d), cm, t);
+        hit = closest_sel(sc, q, cm, t, skip);
       } else {
         sc.count(kCntFullQ, 1);
         hit = query_closest<2>(sc, o, d, t);
@@ -2140,7 +2157,8 @@ RTG_HD int closest_enter(const Scene& sc, const RayQ& q, int h, float& tOut, boo
 // Fused form (sc.fuse & kFuseCone): screen and exact test in one wave-uniform
 // loop in index order (strict <, so the first index still wins ties).
 template <bool kFast, class Scene>
-RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
+RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut,
+                             int skip = -1) {
   float minT = 1000.f;
   int best = -1;
   for (uint64_t m = sel; m;) {  // wave-uniform
@@ -2149,7 +2167,7 @@ RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float
     sc.count(kUSelIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
-    if (!(pass1_rad(q, c, rs) < 0.f)) {
+    if ((int)i != skip && !(pass1_rad(q, c, rs) < 0.f)) {
       sc.count(kCntFullCand, 1);
       sc.count(kUSelExact, 1);
       bool res;
@@ -2162,11 +2180,13 @@ RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float
 }
 
 template <class Scene>
-RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut) {
+RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut,
+                       int skip) {
   if (sc.fuse & kFuseCone) {
-    if (sc.all(q.fast)) return closest_sel_fused<true>(sc, q, sel, tOut);
-    return closest_sel_fused<false>(sc, q, sel, tOut);
+    if (sc.all(q.fast)) return closest_sel_fused<true>(sc, q, sel, tOut, skip);
+    return closest_sel_fused<false>(sc, q, sel, tOut, skip);
   }
+  (void)skip;
   uint64_t cand = 0;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
