@@ -233,10 +233,8 @@ struct DevScene {
   }
   // BVH node nd: four slots {centre, screen radius^2}, their children and
   // containment radii^2 (wave-uniform nd: scalar loads).
-  __device__ __forceinline__ bool has_bvh() const {
-    if constexpr (kBvh) return bvhNodes != nullptr;
-    else return false;
-  }
+  // (the kBvh kernels run only for scenes with a BVH: pick_trace)
+  __device__ __forceinline__ bool has_bvh() const { return kBvh; }
   __device__ __forceinline__ int* bvh_stack() const { return bvhStk; }
   // Sphere lists (BVH scenes): ranges and 32-byte records (one scalar load).
   __device__ __forceinline__ bool has_lists() const {
@@ -334,8 +332,11 @@ struct DevScene {
     return v3(first_lane(v.x), first_lane(v.y), first_lane(v.z));
   }
   // Secondary-ray cone masks (cone_masks, rtg_scene_pack.h): n <= 64.
+  // (BVH scenes have more than 64 spheres: never masks; their kernels drop
+  // the masked paths at compile time)
   __device__ __forceinline__ bool has_cone() const {
     if constexpr (kMasks) return true;
+    else if constexpr (kBvh) return false;
     else return cone != nullptr;
   }
   // Union over the active lanes' origin spheres h (all >= 0) of cone mask
@@ -361,6 +362,7 @@ struct DevScene {
   // Shadow and overlap masks (rtg_scene_pack.h shadow_masks): n <= 64.
   __device__ __forceinline__ bool has_smask() const {
     if constexpr (kMasks) return true;
+    else if constexpr (kBvh) return false;
     else return smask != nullptr;
   }
   __device__ __forceinline__ uint64_t overlap_mask(unsigned h) const {  // per lane
@@ -849,7 +851,7 @@ __device__ __forceinline__ void trace_group(const KernelArgs& a0, Sc& sc, size_t
   if (hasSel) {
     primSel = gsel;
     usePrim = true;
-  } else if (RTG_PROBE_FLOOR < 2 && a.n <= 64) {
+  } else if (RTG_PROBE_FLOOR < 2 && !Sc::kIsBvh && a.n <= 64) {  // (BVH scenes: n > 64)
     float x0, x1, y0, y1;
     // Wave-uniform: do the wave's valid pixels lie in one row?  Then the
     // bounds are four lanes' values, since every float step of main.cpp:
