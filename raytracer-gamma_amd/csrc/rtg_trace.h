@@ -617,7 +617,7 @@ template <class Scene>
 RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT);
 template <class Scene>
 RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h,
-                              unsigned cell, V3 ch, float r2h);
+                              unsigned cell, V3 ch, float r2h, bool& full);
 template <class Scene>
 RTG_HD int closest_bvh(const Scene& sc, const RayQ& q, float& tOut);
 // Most distinct spheres a wave walks the per-sphere lists of (blocked_cap_lanes
@@ -632,7 +632,7 @@ constexpr int kListWalks = RTG_LIST_WALKS;
 #endif
 constexpr int kShadowWalks = RTG_SHADOW_WALKS;
 template <class Scene>
-RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT);
+RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT, bool& full);
 template <class Scene>
 RTG_HD int closest_enter_list(const Scene& sc, const RayQ& q, int h, float& tOut, bool& ok);
 
@@ -687,13 +687,20 @@ RTG_HD V3 matte_light(const Scene& sc, V3 P, V3 N, int hit = -1, bool guardOK = 
           sc.count(kCntShadowQ, 1);
           sc.count(kCntShadowSel, __builtin_popcountll(su));
           blk = blocked_sel(sc, P, dir, gap, su, hit, hc, hr2);
-        } else if (sc.has_lists() && sc.all(guardOK)) {
-          // BVH scene: each lane's hit sphere's capsule list for light l, the
-          // wave's distinct hit spheres in turn (blocked_cap_lanes)
-          if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagShdSame, 1);
-          blk = blocked_cap_lanes(sc, P, dir, gap, l, hit, cell, hc, hr2);
         } else {
-          blk = query_blocked<2>(sc, P, dir, gap);
+          // BVH scene: each lane's hit sphere's capsule list for light l, the
+          // wave's distinct hit spheres in turn (blocked_cap_lanes); the lanes
+          // it leaves, or every lane, take the one full query below (one
+          // inlined BVH traversal per kind keeps the kernel's code small:
+          // DESIGN.md §4 item 66)
+          bool full = true;
+          blk = false;
+          if (sc.has_lists() && sc.all(guardOK)) {
+            if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagShdSame, 1);
+            blk = blocked_cap_lanes(sc, P, dir, gap, l, hit, cell, hc, hr2, full);
+          }
+          if (sc.any(full))
+            if (full) blk = query_blocked<2>(sc, P, dir, gap);
         }
       } else {
         blk = query_blocked<Q>(sc, P, dir, gap);
@@ -818,18 +825,25 @@ RTG_HD int refraction(const Scene& sc, V3 D, V3 P, V3 N, float nSrc, bool wantRa
     sc.count(kCntContainSel, __builtin_popcountll(cu));
     tgt = primary_container_sel(sc, testPt, cu, nTgt);
     if (tgt < 0) tgt = (int)sc.n;  // background material
-  } else if (hit >= 0 && sc.has_lists() &&
-             sc.all(guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax)) {
-    // BVH scene: the first containing sphere of each lane's hit sphere's
-    // overlap list, the wave's distinct hit spheres in turn (container_lanes)
-    if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagContSame, 1);
-    tgt = container_lanes(sc, testPt, hit, nTgt);
-    if (tgt < 0) tgt = (int)sc.n;  // background material
   } else {
-    sc.count(kCntContainFull, 1);
-    tgt = primary_container(sc, testPt);
+    // BVH scene: the first containing sphere of each lane's hit sphere's
+    // overlap list, the wave's distinct hit spheres in turn (container_lanes);
+    // the lanes it leaves, or every lane, take the one full query below
+    bool full = true;
+    tgt = -1;
+    if (hit >= 0 && sc.has_lists() &&
+        sc.all(guardOK && vdot(D, D) <= kContainDirMax * kContainDirMax)) {
+      if (sc.all(sc.first_lane_i(hit) == hit)) sc.count(kUDiagContSame, 1);
+      tgt = container_lanes(sc, testPt, hit, nTgt, full);
+    }
+    if (sc.any(full)) {
+      if (full) {
+        sc.count(kCntContainFull, 1);
+        tgt = primary_container(sc, testPt);
+        nTgt = sc.refr(tgt < 0 ? (int)sc.n : tgt);
+      }
+    }
     if (tgt < 0) tgt = (int)sc.n;  // background material
-    nTgt = sc.refr(tgt);
   }
   sc.probe_end(kProbeSplitContain);
   const float ratio = nSrc / nTgt;
@@ -958,7 +972,11 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     sc.count(kUDiagInsig, significant(I) ? 0 : 1);
     if (sc.all(!significant(I))) sc.count(kUDiagInsigAll, 1);
     sc.probe_begin(kProbeClosest);
-    int hit;
+    int hit = -1;
+    // lanes left for the one full query after the chain below (one inlined
+    // copy of each query kind keeps the kernel's code small: DESIGN.md §4
+    // item 66)
+    bool full = false;
     if (usePrim) {  // the primary ray: only spheres its wave's bundle can reach
       sc.count(kCntPrimQ, 1);
       sc.count(kCntPrimSel, __builtin_popcountll(primSel));
@@ -971,7 +989,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       hit = closest_enter(sc, make_query(o, d), enterH, t, ok);
       sc.count(kCntEnterQ, 1);
       sc.count(kCntEnterOK, ok ? 1 : 0);
-      if (!sc.all(ok)) hit = query_closest<2>(sc, o, d, t);
+      full = !sc.all(ok);
     } else if (Q == 4 && sc.has_cone() && sc.all(originH >= 0)) {
       // secondary rays from sphere origin balls in a narrow bundle: only the
       // spheres of their cone masks for the bundle's cell
@@ -1004,8 +1022,7 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         sc.count(kUQuery, 1);
         hit = closest_sel(sc, q, cm, t, skip);
       } else {
-        sc.count(kCntFullQ, 1);
-        hit = query_closest<2>(sc, o, d, t);
+        full = true;
       }
     } else if (Q == 4 && sc.has_lists() && sc.any(enterH >= 0)) {
       // BVH scene, rays that entered a sphere: each lane's sphere and its
@@ -1031,14 +1048,16 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
           todo = false;
         }
       }
-      if (!done) {
-        sc.count(kCntFullQ, 1);
-        hit = closest_bvh(sc, q, t);
-      }
+      full = !done;
     } else {
       if (sc.has_bvh() && sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
-      sc.count(kCntFullQ, 1);
-      hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
+      full = true;
+    }
+    if (sc.any(full)) {
+      if (full) {
+        sc.count(kCntFullQ, 1);
+        hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
+      }
     }
     enterH = -1;
     originH = -1;
@@ -1846,8 +1865,9 @@ RTG_HD int container_list(const Scene& sc, V3 pt, int h, float& nT) {
 // walk.
 template <class Scene>
 RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l, int h,
-                              unsigned cell, V3 ch, float r2h) {
+                              unsigned cell, V3 ch, float r2h, bool& full) {
   const RayQ q = make_query(o, d);
+  full = false;
   // h itself (every list's first record: capsule_keep's order key) for every
   // lane at once, with the lane's own centre and r^2 (the records' values);
   // the walks then start at each list's second record
@@ -1871,14 +1891,14 @@ RTG_HD bool blocked_cap_lanes(const Scene& sc, V3 o, V3 d, float gap, unsigned l
       todo = false;
     }
   }
-  if (sc.any(todo))
-    if (todo) blk = query_blocked<2>(sc, o, d, gap);
+  full = todo;  // the caller's one BVH query (matte_light)
   return blk;
 }
 template <class Scene>
-RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT) {
+RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT, bool& full) {
   int found = -1;
   bool todo = true;
+  full = false;
   for (int k = 0; k < kListWalks; ++k) {  // wave-uniform
     const int h0 = sc.lane_with(h, todo);
     if (todo && h == h0) {
@@ -1887,11 +1907,7 @@ RTG_HD int container_lanes(const Scene& sc, V3 pt, int h, float& nT) {
     }
     if (!sc.any(todo)) return found;
   }
-  if (todo) {
-    sc.count(kCntContainFull, 1);
-    found = primary_container(sc, pt);
-    nT = sc.refr(found < 0 ? (int)sc.n : found);
-  }
+  full = todo;  // the caller's one full query (refraction)
   return found;
 }
 
