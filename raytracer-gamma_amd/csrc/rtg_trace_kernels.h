@@ -66,18 +66,24 @@ struct LdsFrames {
 // limits their occupancy (7 frame levels + the traversal stack at S = 8: 5
 // waves per SIMD; 6 with this).  Level `top` holds a frame only while a node
 // of depth S - 1 (a leaf) is being shaded below it.
+// RTG_BVH_REG_LEVELS = 2 (A/B builds): the two deepest levels in VGPRs.
+#ifndef RTG_BVH_REG_LEVELS
+#define RTG_BVH_REG_LEVELS 1
+#endif
 template <int kThreads>
 struct LdsFramesTop {
   FrameC* base;  // already offset by threadIdx.x; levels 0 .. top-1
   int top;
-  mutable FrameC reg;
+  mutable FrameC reg[RTG_BVH_REG_LEVELS];
   __device__ __forceinline__ FrameC get(int lv) const {
     const FrameC l = base[(lv < top ? lv : top - 1) * kThreads];
-    return lv < top ? l : reg;
+    if constexpr (RTG_BVH_REG_LEVELS == 1) return lv < top ? l : reg[0];
+    else return lv < top ? l : lv == top ? reg[0] : reg[1];
   }
   __device__ __forceinline__ void set(int lv, const FrameC& v) const {
     if (lv < top) base[lv * kThreads] = v;
-    else reg = v;
+    else if (RTG_BVH_REG_LEVELS == 1 || lv == top) reg[0] = v;
+    else reg[RTG_BVH_REG_LEVELS - 1] = v;
   }
 };
 
@@ -104,7 +110,7 @@ struct DevScene {
   // the deepest of NF levels in VGPRs (LdsFramesTop)
   int nfl;
   __device__ __forceinline__ auto frames() const {
-    if constexpr (kBvh) return LdsFramesTop<kThreads>{lfr, nfl, FrameC{}};
+    if constexpr (kBvh) return LdsFramesTop<kThreads>{lfr, nfl, {}};
     else return LdsFrames<kThreads>{lfr};
   }
   // Diagnostic cycle accounting (kDiag builds only): s_memtime deltas per
@@ -612,7 +618,7 @@ template <int S, int kVariant, bool kBvh = false>
 struct MinWaves {
   static constexpr int value =
       (kVariant == 120) ? 1  // counting build: its counters take registers
-      : (kBvh && (kVariant == 0 || kVariant == 50) && S > 6) ? 6
+      : (kBvh && (kVariant == 0 || kVariant == 50) && S > 6) ? 5 + RTG_BVH_REG_LEVELS
       : (kVariant == 18 && S <= 6) ? 8
       : (kVariant == 0 && S <= 6) ? RTG_DEFAULT_MIN_WAVES
       : ((kVariant % 100 == 0 || kVariant % 100 == 9 || kVariant >= 14) && S <= 6) ? 7 : 1;
@@ -623,7 +629,8 @@ struct MinWaves {
 // (LdsFramesTop keeps the deepest in VGPRs).  launch_trace sizes the LDS with
 // the same rule.
 constexpr int frame_lds_levels(int S, bool bvh) {
-  return (S > 1 ? S - 1 : 1) - ((bvh && S >= 3) ? 1 : 0);
+  return (S > 1 ? S - 1 : 1) -
+         (!bvh || S < 3 ? 0 : S < 4 ? 1 : RTG_BVH_REG_LEVELS);
 }
 
 // Workgroup prologue: the frame area and (kLds) the scene tables staged in LDS.
