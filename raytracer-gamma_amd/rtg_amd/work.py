@@ -111,46 +111,46 @@ UNIT_COST = {
 # and 10 seeded BVH scenes; least squares on the relative residuals with a
 # ridge toward the source prices and bounds of 0.6-1.7x the SOURCE prices
 # (never an earlier fit's, so refits do not drift: ADVICE r05).  rms model/PMC
-# error over the set: source prices 7.9 %, fitted 2.6 % (in sample).
-# Held out, each bench config left out of its own fit: c2 0.991, c3 1.016, c4 0.985, c5 1.013;
-# a fit on the seeded scenes alone: c2 1.044, c3 1.061, c4 1.026, c5 1.020 (FIT_RECORD).
+# error over the set: source prices 10.4 %, fitted 2.7 % (in sample).
+# Held out, each bench config left out of its own fit: c2 0.993, c3 1.011, c4 0.982, c5 1.010;
+# a fit on the seeded scenes alone: c2 1.012, c3 1.018, c4 0.994, c5 1.013 (FIT_RECORD).
 FIT_RECORD = "profiles/r06/calib_units/fit.json"
 UNIT_COST_SOURCE = dict(UNIT_COST)
 UNIT_COST.update({
-    "U.query": 17.27,
-    "U.primIter": 11.32,
-    "U.primExact": 46.15,
-    "U.selIter": 9.91,
-    "U.selExact": 44.86,
-    "U.shdIter": 11.08,
-    "U.shdExact": 54.91,
-    "U.enterHead": 78.89,
-    "U.enterIter": 2.95,
-    "U.enterExact": 35.12,
-    "U.fullGroup": 54.73,
-    "U.fullExact": 81.17,
-    "U.bvhNode": 2.02,
-    "U.bvhSlot": 27.97,
-    "U.bvhExact": 62.4,
-    "U.contIter": 12.53,
-    "U.contBvhNode": 47.09,
-    "U.cone": 16.24,
+    "U.query": 19.9,
+    "U.primIter": 11.59,
+    "U.primExact": 48.41,
+    "U.selIter": 11.39,
+    "U.selExact": 55.88,
+    "U.shdIter": 13.44,
+    "U.shdExact": 57.26,
+    "U.enterHead": 81.19,
+    "U.enterIter": 2.97,
+    "U.enterExact": 39.51,
+    "U.fullGroup": 50.96,
+    "U.fullExact": 81.2,
+    "U.bvhNode": 2.0,
+    "U.bvhSlot": 20.37,
+    "U.bvhExact": 59.36,
+    "U.contIter": 12.83,
+    "U.contBvhNode": 47.32,
+    "U.cone": 16.78,
     "U.maskIter": 4.02,
-    "U.node": 13.01,
-    "U.shade": 75.1,
-    "U.light": 10.15,
-    "U.lightDir": 27.88,
-    "U.shadow": 2.97,
-    "U.lit": 15.53,
-    "U.refr": 189.11,
-    "U.refrLeaf": 259.77,
-    "U.push": 46.93,
-    "U.descend": 27.36,
-    "U.unwind": 11.77,
-    "U.capIter": 13.11,
-    "U.ovIter": 11.96,
-    "U.sample": 133.02,
-    "U.wave": 27.22,
+    "U.node": 13.37,
+    "U.shade": 81.97,
+    "U.light": 12.77,
+    "U.lightDir": 35.71,
+    "U.shadow": 3.06,
+    "U.lit": 17.77,
+    "U.refr": 219.43,
+    "U.refrLeaf": 271.0,
+    "U.push": 49.64,
+    "U.descend": 27.72,
+    "U.unwind": 11.91,
+    "U.capIter": 10.34,
+    "U.ovIter": 11.18,
+    "U.sample": 136.0,
+    "U.wave": 26.58,
 })
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # one wave64 VALU op per 2 cycles per SIMD
