@@ -162,6 +162,12 @@ constexpr size_t kStatSet = (size_t)kListParts * kStatStride;
 // the C2 pass took 21 us, 11 of them queued atomics.  Once they no longer
 // queue, one group per lane beats the 2 or 4 per lane that had kept the
 // block count down (C3 pass 39 -> 31 us, C4 frame -1 %).
+// The trace kernel's one-wave workgroups w take partition w % kListParts, so
+// block b's groups are traced on the XCD that ran block b (both b mod 8) and
+// find its list entries, cost-table reads and zero-filled lines in that XCD's
+// L2.  Measured (profiles/r06/partition_map/): partition (b + b/16) % 16,
+// which spreads a partition over all XCDs, C2 +4.5 %, C3 +6.5 %, C4 +4 %; a
+// skew within each XCD's two partitions still +1.2-3.4 %.
 // Each listed group's sphere mask goes to groupSel at the same list index:
 // the trace kernel takes it as the wave's primary-ray subset (one scalar
 // load) instead of recomputing the cull.

@@ -989,7 +989,10 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
       hit = closest_enter(sc, make_query(o, d), enterH, t, ok);
       sc.count(kCntEnterQ, 1);
       sc.count(kCntEnterOK, ok ? 1 : 0);
-      full = !sc.all(ok);
+      if (!sc.all(ok)) {  // masked scenes only: a query site of its own
+        sc.count(kCntFullQ, 1);
+        hit = query_closest<2>(sc, o, d, t);
+      }
     } else if (Q == 4 && sc.has_cone() && sc.all(originH >= 0)) {
       // secondary rays from sphere origin balls in a narrow bundle: only the
       // spheres of their cone masks for the bundle's cell
@@ -1021,8 +1024,9 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         sc.count(kCntConeSel, __builtin_popcountll(cm));
         sc.count(kUQuery, 1);
         hit = closest_sel(sc, q, cm, t, skip);
-      } else {
-        full = true;
+      } else {  // masked scenes only: a query site of its own
+        sc.count(kCntFullQ, 1);
+        hit = query_closest<2>(sc, o, d, t);
       }
     } else if (Q == 4 && sc.has_lists() && sc.any(enterH >= 0)) {
       // BVH scene, rays that entered a sphere: each lane's sphere and its
@@ -1049,8 +1053,11 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
         }
       }
       full = !done;
+    } else if (!sc.has_bvh()) {  // masked and flat scenes: a query site of its own
+      sc.count(kCntFullQ, 1);
+      hit = query_closest<Q == 4 ? 2 : Q>(sc, o, d, t);
     } else {
-      if (sc.has_bvh() && sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
+      if (sc.all(enterH >= 0)) sc.count(kUDiagEnterAll, 1);
       full = true;
     }
     if (sc.any(full)) {
