@@ -150,22 +150,7 @@ RTG_HD float cull_rsq(float x) {
   return 1.0f / sqrtf(x);
 #endif
 }
-#ifndef RTG_FLAT_UNWIND
-#define RTG_FLAT_UNWIND 0
-#endif
 RTG_HD float rtg_sqrtf(float x) { return sqrt_rn(x); }
-// m &= ~(1 << i) for a wave-uniform mask walked lowest bit first: one
-// s_bitset0_b64 (the compiler's form is a 64-bit shift and an and-not).
-#ifndef RTG_BITSET0
-#define RTG_BITSET0 0
-#endif
-RTG_HD void clear_bit(uint64_t& m, unsigned i) {
-#if defined(__HIP_DEVICE_COMPILE__) && RTG_BITSET0
-  asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));
-#else
-  m &= ~(1ull << i);
-#endif
-}
 // rcp_rn(sqrt_rn(x)) with ONE range check: for x in sqrt_fast's range the
 // rounded root lies in [2^-48, 2^64], inside rcp_fast's, so both short
 // sequences hold; outside it, both compiler sequences (same results).
@@ -532,7 +517,7 @@ RTG_HD int primary_container_sel(const Scene& sc, V3 pt, uint64_t sel, float& nT
   nT = sc.refr((int)sc.n);  // background material (wave-uniform: scalar load)
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, i);
+    m &= ~(1ull << i);  // (an asm s_bitset0_b64: neutral)
     sc.count(kUContIter, 1);
     float cr;
     const V3 c = sc.sphere_contain(i, cr);
@@ -1198,49 +1183,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
 
     // ---------------- unwind (stages 1 and 2) ----------------
     sc.probe_begin(kProbeUnwind);
-#if RTG_FLAT_UNWIND
-    // The lane's unwind state as an integer in a VGPR (1: unwinding, 2:
-    // descends into a reflection child, 0: done) and a wave-uniform loop: a
-    // divergent loop exit keeps its flags as lane masks in SGPRs, merged by
-    // three scalar instructions each per iteration.
-    int ust = sp > 0 ? 1 : 0;
-    while (sc.any(ust == 1)) {  // wave-uniform
-      if (ust == 1) {
-        sc.count(kUUnwind, 1);
-        const int lv = sp - 1 < NF ? sp - 1 : NF - 1;
-        FrameC f = fc.get(lv);
-        const V3 fcol = vadd(ret, v3(f.cx, f.cy, f.cz));        // :553 / :622
-        ret = fcol;                                             // :617 / :626
-        const bool st2 = (f.meta & 3u) == 2u;                   // stage 1, reflection
-        if (st2) {
-          f.cx = fcol.x; f.cy = fcol.y; f.cz = fcol.z;
-          f.meta = (f.meta & ~3u) | 1u;                         // -> stage 2
-          fc.set(lv, f);
-          const FrameR r = load_frame_r<IsBvhScene<Scene>::value>(fr[lv]);
-          o = r.ro; d = r.rd; I = r.rI; rm = (int)(f.meta >> 10);
-          originH = (int)((f.meta >> 2) & 0x7Fu) - 1;
-          if (Q == 4 && (f.meta & 0x200u)) enterH = originH;  // reflection back into it
-#if RTG_BVH_INSIDE
-          if constexpr (Q == 4 && IsBvhScene<Scene>::value) {
-            if (sc.n < 2048u) {
-              rm = (int)(f.meta >> 21);
-              originH = -1;
-              enterH = (f.meta & 0x200u) ? (int)((f.meta >> 10) & 0x7FFu) - 1 : -1;
-            }
-          }
-#endif
-          if constexpr (kCL) ret = v3(0.f, 0.f, 0.f);           // raytrace_kernel.cl:845
-        }
-        sp = st2 ? sp : sp - 1;
-        ust = st2 ? 2 : (sp > 0 ? 1 : 0);
-      }
-#if defined(__HIP_DEVICE_COMPILE__)
-      asm("" : "+v"(ust));
-#endif
-    }
-    sc.probe_end(kProbeUnwind);
-    if (ust != 2) return ret;
-#else
     bool descend = false;
     while (sp > 0) {
       sc.count(kUUnwind, 1);
@@ -1273,7 +1215,6 @@ RTG_HD V3 trace_sample(const Scene& sc, V3 dir0, FStore&& fc, bool usePrim = fal
     }
     sc.probe_end(kProbeUnwind);
     if (!descend) return ret;
-#endif
   }
 }
 
@@ -2078,7 +2019,7 @@ RTG_HD bool blocked_sel_fused(const Scene& sc, const RayQ& q, float gap, uint64_
   unsigned blkv = 0u;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, i);
+    m &= ~(1ull << i);
     sc.count(kUShdIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
@@ -2188,7 +2129,7 @@ RTG_HD int closest_enter_fused(const Scene& sc, const RayQ& q, int h, float& tOu
   int best = h;
   for (uint64_t m = u; m;) {  // wave-uniform
     const unsigned j = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, j);
+    m &= ~(1ull << j);
     sc.count(kUEnterIter, 1);
     float rj2;
     const V3 cj = sc.sphere(j, rj2);
@@ -2253,7 +2194,7 @@ RTG_HD int closest_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, float
   int best = -1;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, i);
+    m &= ~(1ull << i);
     sc.count(kUSelIter, 1);
     float rs, r2, ocu;
     const V3 c = sc.sphere_fused(i, rs, r2, ocu);
@@ -2280,7 +2221,7 @@ RTG_HD int closest_sel(const Scene& sc, const RayQ& q, uint64_t sel, float& tOut
   uint64_t cand = 0;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, i);
+    m &= ~(1ull << i);
     float rs;
     const V3 c = sc.sphere_screen(i, rs);
     cand |= (pass1_rad(q, c, rs) < 0.f) ? 0ull : (1ull << i);
@@ -2315,7 +2256,7 @@ RTG_HD int closest_hit_sel_fused(const Scene& sc, const RayQ& q, uint64_t sel, f
   const V3 d = q.d;
   for (uint64_t m = sel; m;) {  // wave-uniform
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, i);
+    m &= ~(1ull << i);
     sc.count(kUPrimIter, 1);
     float rs, r2, oc;
     const V3 c = sc.sphere_fused(i, rs, r2, oc);
@@ -2355,7 +2296,7 @@ RTG_HD int closest_hit_sel(const Scene& sc, V3 o, V3 d, float& tOut, uint64_t se
   uint64_t cand = 0;
   for (uint64_t m = sel; m;) {  // wave-uniform: scalar loop + scalar loads
     const unsigned i = (unsigned)__builtin_ctzll(m);
-    clear_bit(m, i);
+    m &= ~(1ull << i);
     float r2;
     const V3 c = sc.sphere(i, r2);
     const float b = 2.0f * vdot(d, c);
