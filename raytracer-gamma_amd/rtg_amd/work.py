@@ -112,45 +112,45 @@ UNIT_COST = {
 # ridge toward the source prices and bounds of 0.6-1.7x the SOURCE prices
 # (never an earlier fit's, so refits do not drift: ADVICE r05).  rms model/PMC
 # error over the set: source prices 10.4 %, fitted 2.7 % (in sample).
-# Held out, each bench config left out of its own fit: c2 0.993, c3 1.011, c4 0.982, c5 1.010;
-# a fit on the seeded scenes alone: c2 1.012, c3 1.018, c4 0.994, c5 1.013 (FIT_RECORD).
+# Held out, each bench config left out of its own fit: c2 0.992, c3 1.011, c4 0.982, c5 1.010;
+# a fit on the seeded scenes alone: c2 1.009, c3 1.016, c4 0.993, c5 1.013 (FIT_RECORD).
 FIT_RECORD = "profiles/r06/calib_units/fit.json"
 UNIT_COST_SOURCE = dict(UNIT_COST)
 UNIT_COST.update({
-    "U.query": 19.9,
-    "U.primIter": 11.59,
-    "U.primExact": 48.41,
-    "U.selIter": 11.39,
-    "U.selExact": 55.88,
-    "U.shdIter": 13.44,
-    "U.shdExact": 57.26,
-    "U.enterHead": 81.19,
+    "U.query": 19.97,
+    "U.primIter": 11.58,
+    "U.primExact": 48.38,
+    "U.selIter": 11.43,
+    "U.selExact": 55.98,
+    "U.shdIter": 13.54,
+    "U.shdExact": 57.52,
+    "U.enterHead": 81.57,
     "U.enterIter": 2.97,
-    "U.enterExact": 39.51,
-    "U.fullGroup": 50.96,
-    "U.fullExact": 81.2,
+    "U.enterExact": 39.09,
+    "U.fullGroup": 50.98,
+    "U.fullExact": 81.25,
     "U.bvhNode": 2.0,
-    "U.bvhSlot": 20.37,
-    "U.bvhExact": 59.36,
-    "U.contIter": 12.83,
+    "U.bvhSlot": 20.39,
+    "U.bvhExact": 59.4,
+    "U.contIter": 12.8,
     "U.contBvhNode": 47.32,
-    "U.cone": 16.78,
+    "U.cone": 16.8,
     "U.maskIter": 4.02,
     "U.node": 13.37,
-    "U.shade": 81.97,
-    "U.light": 12.77,
-    "U.lightDir": 35.71,
+    "U.shade": 81.94,
+    "U.light": 12.84,
+    "U.lightDir": 35.96,
     "U.shadow": 3.06,
-    "U.lit": 17.77,
-    "U.refr": 219.43,
-    "U.refrLeaf": 271.0,
-    "U.push": 49.64,
-    "U.descend": 27.72,
-    "U.unwind": 11.91,
-    "U.capIter": 10.34,
-    "U.ovIter": 11.18,
+    "U.lit": 17.88,
+    "U.refr": 216.57,
+    "U.refrLeaf": 270.71,
+    "U.push": 50.08,
+    "U.descend": 27.69,
+    "U.unwind": 11.92,
+    "U.capIter": 10.3,
+    "U.ovIter": 11.19,
     "U.sample": 136.0,
-    "U.wave": 26.58,
+    "U.wave": 26.08,
 })
 
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # one wave64 VALU op per 2 cycles per SIMD
