@@ -148,6 +148,14 @@ __device__ __forceinline__ uint64_t group_sel(const KernelArgs& a, size_t g, uns
   return sel;
 }
 
+// Launches of at most this many pixel groups list them in eight runs
+// (KernelArgs::nRuns): a 1/8 or 1/4 C3 shard's chunks (~60 k, ~125 k), not a
+// whole C2 frame (292 k).
+#ifndef RTG_RUNS8_MAX_GROUPS
+#define RTG_RUNS8_MAX_GROUPS 200000
+#endif
+constexpr size_t kRuns8MaxGroups = RTG_RUNS8_MAX_GROUPS;
+
 // One launch's counter sets: the run lengths and the cost sums of all list
 // partitions (KernelArgs::groupCount, costStat).
 constexpr size_t kCountSet = (size_t)kListParts * kCountStride;
@@ -192,12 +200,14 @@ constexpr size_t kStatSet = (size_t)kListParts * kStatStride;
 // Partition p's region is [2 p cap, 2 (p + 1) cap) (cap = a.groupCap, the
 // groups of the partition's blocks): run 0 fills its first half from the
 // front, run 1 from the back, runs 2 and 3 the second half likewise.
+template <unsigned kRuns>
 __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, size_t nGroups,
                                                           unsigned* groupList,
                                                           unsigned long long* groupSel,
                                                           unsigned* groupCount) {
-  __shared__ unsigned cnt[4][4];
-  __shared__ unsigned blockBase[4];
+  static_assert(kRuns == 4 || kRuns == 8, "four or eight runs");
+  __shared__ unsigned cnt[kRuns][4];
+  __shared__ unsigned blockBase[kRuns];
   __shared__ unsigned long long waveCost[4];
   const unsigned lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const unsigned part = blockIdx.x % kListParts;
@@ -236,13 +246,17 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   unsigned run;
   if (mu > 0.f) {
     const float c = (float)cost;
-    run = c >= 2.f * mu ? 0u : c >= mu ? 1u : c >= 0.5f * mu ? 2u : 3u;
+    if constexpr (kRuns == 8)  // short launches (KernelArgs::nRuns): finer longest-first order
+      run = c >= 3.f * mu ? 0u : c >= 2.f * mu ? 1u : c >= 1.5f * mu ? 2u : c >= mu ? 3u
+          : c >= 0.75f * mu ? 4u : c >= 0.5f * mu ? 5u : c >= 0.25f * mu ? 6u : 7u;
+    else
+      run = c >= 2.f * mu ? 0u : c >= mu ? 1u : c >= 0.5f * mu ? 2u : 3u;
   } else {
     run = pc >= a.lptMin ? 0u : 1u;
   }
-  uint64_t live[4];
+  uint64_t live[kRuns];
 #pragma unroll
-  for (unsigned c = 0; c < 4; ++c) {
+  for (unsigned c = 0; c < kRuns; ++c) {
     live[c] = __ballot(pc != 0u && run == c);
     if (lane == 0) cnt[c][wave] = (unsigned)__builtin_popcountll(live[c]);
   }
@@ -252,7 +266,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
     if (lane == 0) waveCost[wave] = costAcc;
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < kRuns) {
     const unsigned c = threadIdx.x;
     const unsigned sum = cnt[c][0] + cnt[c][1] + cnt[c][2] + cnt[c][3];
     blockBase[c] = sum ? atomicAdd(&groupCount[part * kCountStride + c], sum) : 0u;
@@ -262,16 +276,18 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(const KernelArgs a, si
   }
   __syncthreads();
   const unsigned cap = a.groupCap;
-  const size_t region = (size_t)part * 2u * cap;
+  // runs 2k and 2k + 1 share [k cap, (k + 1) cap): the even one from the
+  // front, the odd one from the back
+  const size_t region = (size_t)part * (kRuns / 2u) * cap;
 #pragma unroll
-  for (unsigned c = 0; c < 4; ++c) {
+  for (unsigned c = 0; c < kRuns; ++c) {
     const uint64_t m = live[c];
     if ((m >> lane) & 1ull) {
       unsigned off = blockBase[c];  // list order: (wave, lane)
       for (unsigned w = 0; w < wave; ++w) off += cnt[c][w];
       const unsigned r = off + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      const unsigned at = c == 0 ? r : c == 1 ? cap - 1u - r : c == 2 ? cap + r : 2u * cap - 1u - r;
+      const unsigned at = (c >> 1) * cap + ((c & 1u) ? cap - 1u - r : r);
       groupList[region + at] = (unsigned)g;
       groupSel[region + at] = sel;
     }
@@ -368,6 +384,7 @@ struct rtg_context {
   int lastSlot = -1;
   size_t lastGroups = 0;
   size_t lastPartCap = 0;
+  unsigned lastRuns = 4;
   int lastCost = -1;
   rtg_launch_opts opts{};
   int semantics = RTG_SEMANTICS_CPU;
@@ -608,10 +625,12 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
   std::vector<unsigned> cnt(kCountSet);
   HIP_TRY(hipMemcpy(cnt.data(), slot.count + kCountSet * (1 - slot.parity),
                     kCountSet * sizeof(unsigned), hipMemcpyDeviceToHost));
+  const unsigned nR = ctx->lastRuns;  // 4 or 8 runs (eight: reported in pairs)
   if (runs)
     for (unsigned c = 0; c < 4; ++c) {
       runs[c] = 0;
-      for (unsigned p = 0; p < kListParts; ++p) runs[c] += cnt[p * kCountStride + c];
+      for (unsigned p = 0; p < kListParts; ++p)
+        for (unsigned k = c * nR / 4; k < (c + 1) * nR / 4; ++k) runs[c] += cnt[p * kCountStride + k];
     }
   if (!list && !sel) return RTG_OK;
   std::vector<unsigned> l(slot.cap);
@@ -626,7 +645,8 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
   unsigned tot[kListParts];
   for (unsigned p = 0; p < kListParts; ++p) {
     const unsigned* g = &cnt[p * kCountStride];
-    tot[p] = g[0] + g[1] + g[2] + g[3];
+    tot[p] = 0;
+    for (unsigned k = 0; k < nR; ++k) tot[p] += g[k];
     if (tot[p] > most) most = tot[p];
   }
   size_t out = 0;
@@ -635,10 +655,10 @@ int rtg_diag_group_list(rtg_context* ctx, unsigned* cost, unsigned* list,
     const size_t j = t / kListParts;
     if (j >= tot[p]) continue;
     const unsigned* g = &cnt[p * kCountStride];
-    const size_t e0 = g[0], e1 = e0 + g[1], e2 = e1 + g[2];
-    const size_t r = j < e0 ? j : j < e1 ? pc - 1 - (j - e0) : j < e2 ? pc + (j - e1)
-                                                              : 2 * pc - 1 - (j - e2);
-    const size_t at = 2 * pc * p + r;
+    size_t jr = j, c = 0;  // run c, its entry jr
+    while (jr >= g[c]) jr -= g[c++];
+    const size_t r = (c >> 1) * pc + ((c & 1) ? pc - 1 - jr : jr);
+    const size_t at = (nR / 2) * pc * p + r;
     if (list) list[out] = l[at];
     if (sel) sel[out] = m[at];
     ++out;
@@ -904,6 +924,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
   a.groupSel = nullptr;
   a.groupCount = nullptr;
   a.groupCap = 0;
+  a.nRuns = 4;
   a.lptMin = (unsigned)ctx->lptMin;
   a.nPersist = 0;
   a.groupCost = nullptr;
@@ -952,7 +973,10 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     // each list partition's capacity: the groups of its cull-pass blocks
     const size_t cullBlocks = (groups + 255) / 256;
     const size_t partCap = (cullBlocks + kListParts - 1) / kListParts * 256;
-    const size_t listCap = 2 * kListParts * partCap;  // list entries (KernelArgs::groupCap)
+    // short launches (a multi-GPU frame's shard chunks) list their groups in
+    // eight longest-first runs, whole frames in four
+    const unsigned nRuns = groups <= kRuns8MaxGroups ? 8u : 4u;
+    const size_t listCap = (nRuns / 2) * kListParts * partCap;  // list entries (KernelArgs::groupCap)
     if (compact && ctx->n <= 64 && listCap < 0xFFFFFFFFull) {
       listed = true;
       const hipStream_t st = (hipStream_t)stream;
@@ -1045,6 +1069,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
       a.groupCount = slot->count + kCountSet * slot->parity;
       a.zeroCount = slot->count + kCountSet * (1 - slot->parity);  // parity flips at the commit
       a.groupCap = (unsigned)partCap;
+      a.nRuns = nRuns;
       // a multiple of kListParts (wave w takes list partition w % kListParts)
       const size_t np = groups < persist ? groups : persist;
       a.nPersist = (unsigned)((np + kListParts - 1) / kListParts * kListParts);
@@ -1090,6 +1115,7 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     ctx->lastSlot = slotIdx;
     ctx->lastGroups = cullGroups;
     ctx->lastPartCap = a.groupCap;
+    ctx->lastRuns = a.nRuns;
     ctx->lastCost = costEntry ? (int)(costEntry - ctx->costs) : -1;
   }
   if (costEntry) {
@@ -1108,8 +1134,12 @@ static int launch_trace(rtg_context* ctx, unsigned width, unsigned height, float
     const hipStream_t st = (hipStream_t)stream;
     const dim3 cgrid((unsigned)((cullGroups + 255) / 256));
     unsigned* cnt = const_cast<unsigned*>(a.groupCount);
-    hipLaunchKernelGGL(cull_groups_kernel, cgrid, dim3(256), 0, st, a, cullGroups, slot->list,
-                       slot->sel, cnt);
+    if (a.nRuns == 8)
+      hipLaunchKernelGGL(cull_groups_kernel<8>, cgrid, dim3(256), 0, st, a, cullGroups,
+                         slot->list, slot->sel, cnt);
+    else
+      hipLaunchKernelGGL(cull_groups_kernel<4>, cgrid, dim3(256), 0, st, a, cullGroups,
+                         slot->list, slot->sel, cnt);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
       hipLaunchKernelGGL(fn, grid, dim3(threads), lds, st, a);

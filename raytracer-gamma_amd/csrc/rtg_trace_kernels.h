@@ -544,6 +544,7 @@ struct KernelArgs {
   // Partition p's run lengths are groupCount[p kCountStride + 0..3].
   const unsigned* groupCount;
   unsigned groupCap;
+  unsigned nRuns;              // the list's longest-first runs: 4, or 8 for short launches
   unsigned lptMin;             // cull_groups_kernel's popcount threshold (no cost feedback)
   unsigned nPersist;
   // Launch-order feedback (compacted launches; null when off): each listed
@@ -1027,6 +1028,16 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
       const RTG_CONST unsigned* gc =
           (const RTG_CONST unsigned*)b->groupCount + part * kCountStride;
       const unsigned cap = b->groupCap;
+      if (b->nRuns == 8u) {  // short launches: runs 2k, 2k + 1 share [k cap, (k + 1) cap)
+        unsigned jr = j;
+#pragma unroll
+        for (unsigned c = 0; c < 8u; ++c) {
+          const unsigned n = gc[c];
+          if (jr < n) return 4u * cap * part + (c >> 1) * cap + ((c & 1u) ? cap - 1u - jr : jr);
+          jr -= n;
+        }
+        return ~0u;
+      }
       const unsigned e0 = gc[0], e1 = e0 + gc[1], e2 = e1 + gc[2], e3 = e2 + gc[3];
       const unsigned r = j < e0 ? j
                        : j < e1 ? cap - 1u - (j - e0)
@@ -1041,6 +1052,7 @@ __device__ __forceinline__ void trace_samples_body(const KernelArgs& a) {
       const unsigned l = threadIdx.x & 63u;
       if (l < kListParts) {
         *(uint4*)(b->zeroCount + l * kCountStride) = make_uint4(0u, 0u, 0u, 0u);
+        *(uint4*)(b->zeroCount + l * kCountStride + 4) = make_uint4(0u, 0u, 0u, 0u);
         if (unsigned long long* zs = b->zeroStat) zs[l * kStatStride] = 0ull;
       }
     }
