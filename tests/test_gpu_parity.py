@@ -388,15 +388,17 @@ def test_failed_launch_leaves_slots_consistent(R, golden, torch_cuda):
     ctx.close()
 
 
-def test_group_list_partitions(R, golden, torch_cuda):
+@pytest.mark.parametrize("name", ["c2", "c1"])
+def test_group_list_partitions(R, golden, torch_cuda, name):
     """The compacted launch's list (cull_groups_kernel: kListParts partitions,
-    each with its own run counters): over a cold launch, a launch whose cull
-    pass sums the cost table and a launch ordered by it, every listed group
-    appears once, has a non-empty sphere mask, and every group with a non-zero
-    pixel is listed (the others were zero-filled by the cull pass)."""
+    each with its own run counters; four runs for a whole C2 frame, eight for
+    C1's short launch): over a cold launch, a launch whose cull pass sums the
+    cost table and a launch ordered by it, every listed group appears once, has
+    a non-empty sphere mask, and every group with a non-zero pixel is listed
+    (the others were zero-filled by the cull pass)."""
     torch = torch_cuda
-    c = golden["configs"]["c2"]
-    sph, lg = load_scene("c2", c["spheres"], c["lights"])
+    c = golden["configs"][name]
+    sph, lg = load_scene(name, c["spheres"], c["lights"])
     W, H, S = c["W"], c["H"], c["stack_size"]
     ctx = R.Context(0)
     ctx.set_scene(sph, lg)
